@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Headline benchmark: chunks/sec of the VGGT encoder (Aggregator: DINOv2
+ViT-L/14-reg + 24 frame + 24 global alternating-attention blocks) forward on
+one 16-frame 518x518 synthetic chunk (BASELINE.json configs[1]), bf16 MFMA,
+random-init weights.
+
+  python bench.py [--gpus N --steps K --warmup W] [--workload aggregator|chunk]
+
+N > 1: one process per GPU (torch.distributed over RCCL, launched by
+torch.distributed.run); every rank runs its own independent chunks (the
+encoder does not shard -- replicas, weak scaling), value = all ranks' chunks
+/ max-over-ranks time.  Prints ONE JSON line on rank 0 with the roofline of
+the dominant kernel (global attention) measured with HIP events on the
+stream it is launched on, and the CPU baseline (the oracle's fp32 path on a
+bounded sample of the same workload).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "large-scale-vit-slam_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+H_IMG = W_IMG = 518
+S_FRAMES = 16
+
+
+def agg_flops(S=S_FRAMES, H=H_IMG, W=W_IMG, C=1024, depth=24, dino_depth=24):
+    """Algorithmic FLOPs of one aggregator forward (BASELINE.md §2 counting:
+    2MNK per GEMM, 4*Nq*Nk*d per attention)."""
+    hw = (H // 14) * (W // 14)
+    P = 5 + hw
+    T = S * P
+    lin_per_block = 24 * T * C * C  # qkv 6, proj 2, fc1 8, fc2 8 (x T C^2)
+    frame_attn = 4 * S * P * P * C
+    global_attn = 4 * T * T * C
+    patch = 2 * S * hw * 3 * 14 * 14 * C
+    total = (depth * 2 + dino_depth) * lin_per_block + (dino_depth + depth) * frame_attn + depth * global_attn + patch
+    return {"total": total, "global_attn_launch": global_attn, "global_attn": depth * global_attn,
+            "attn": depth * global_attn + (dino_depth + depth) * frame_attn}
+
+
+def cpu_baseline(threads: int):
+    """Time the oracle (reference numerics, fp32, CPU) on a bounded sample of
+    the SAME workload: one DINOv2 block, one frame block and one global block
+    at the full 16x518x518 chunk shape; scale to a whole chunk by the layer
+    counts (24 each; patch-embed/LN glue < 0.1% of FLOPs is not counted)."""
+    from oracle import vggt_oracle as O
+    from aligned_vggt.backbone.aggregator import Aggregator
+    from aligned_vggt.utils.synthetic import synthetic_init_
+    torch.set_num_threads(threads)
+    agg = Aggregator(depth=1, dino_depth=1)
+    synthetic_init_(agg)
+    sd = {"aggregator." + k: v for k, v in agg.state_dict().items()}
+    hw = (H_IMG // 14) * (W_IMG // 14)
+    P = 5 + hw
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(S_FRAMES, P, 1024, generator=g)
+    pos = O.position_grid(S_FRAMES, H_IMG // 14, W_IMG // 14, 5)
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        O.block(sd, "aggregator.patch_embed.blocks.0.", x, 16, eps=1e-6)
+        t1 = time.perf_counter()
+        O.block(sd, "aggregator.frame_blocks.0.", x, 16, pos, "2d", True)
+        t2 = time.perf_counter()
+        O.block(sd, "aggregator.global_blocks.0.", x.view(1, S_FRAMES * P, 1024), 16, pos.view(1, -1, 2), "2d", True)
+        t3 = time.perf_counter()
+    sec_chunk = 24 * (t1 - t0) + 24 * (t2 - t1) + 24 * (t3 - t2)
+    return {"value": 1.0 / sec_chunk, "unit": "chunks/s", "cores": threads, "kind": "port",
+            "sample": f"oracle fp32 CPU (reference numerics): 1 DINOv2 + 1 frame + 1 global block at 16x518x518 "
+                      f"({t3 - t0:.1f} s measured), scaled x24 each to a full aggregator chunk "
+                      f"({sec_chunk:.1f} s/chunk)"}
+
+
+class EventTimer:
+    """HIP-event timing of tagged native launches on the launching stream."""
+
+    def __init__(self, tags):
+        self.tags = set(tags)
+        self.pairs = []
+        self.active = False
+
+    def __call__(self, tag, fn):
+        if not self.active or tag not in self.tags:
+            return fn()
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        st = torch.cuda.current_stream()
+        s.record(st)
+        r = fn()
+        e.record(st)
+        self.pairs.append((s, e))
+        return r
+
+    def mean_ms(self):
+        torch.cuda.synchronize()
+        if not self.pairs:
+            return None
+        return sum(s.elapsed_time(e) for s, e in self.pairs) / len(self.pairs)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="aggregator", choices=["aggregator"])
+    ap.add_argument("--frames", type=int, default=S_FRAMES)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from aligned_vggt import _native
+    from aligned_vggt.backbone.aggregator import Aggregator
+    from aligned_vggt.utils.synthetic import synthetic_images, synthetic_init_
+
+    agg = Aggregator().to(dev)
+    synthetic_init_(agg, seed=0)
+    agg.eval()
+    imgs = synthetic_images(1, args.frames, H_IMG, W_IMG, seed=1234 + rank, device=dev)
+    keep = (4, 11, 17, 23)
+
+    timer = EventTimer({"global_attn"})
+    _native.EVENT_HOOK = timer
+
+    def step():
+        outs, _ = agg(imgs, keep_layers=keep)
+        return outs
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timer.active = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    timer.active = False
+    attn_ms = timer.mean_ms()
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+
+    fl = agg_flops(S=args.frames)
+    chunks = args.steps * world
+    value = chunks / dt
+    ms_step = dt / args.steps * 1e3
+    if rank == 0:
+        attn_tflops = fl["global_attn_launch"] / (attn_ms * 1e-3) / 1e12 if attn_ms else None
+        line = {
+            "metric": "chunks/sec (16-frame 518x518) + ViT MFMA util%",
+            "value": round(value, 4),
+            "unit": "chunks/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (uniform [0,1) frames, random-init weights)",
+            "config": {"workload": "VGGT aggregator forward (DINOv2-L/14-reg + 24x frame/global AA blocks), "
+                                   "1 chunk of %d frames 518x518, layers 4/11/17/23 emitted" % args.frames,
+                       "frames": args.frames, "tokens_per_chunk": args.frames * (5 + 37 * 37),
+                       "parallelism": "replicas x%d" % world},
+            "mfma_util_whole_step": round(fl["total"] * value / world / (PEAK_BF16_TFLOPS * 1e12), 4),
+            "tflops_per_gpu": round(fl["total"] * value / world / 1e12, 1),
+            "roofline": {"bound": "mfma", "kernel": "attn_fwd_kernel<64> (global attention, 1x16 heads x 21984^2 x 64)",
+                         "achieved": round(attn_tflops, 1) if attn_tflops else None, "peak": PEAK_BF16_TFLOPS,
+                         "unit": "TFLOP/s",
+                         "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4) if attn_tflops else None,
+                         "avg_launch_ms": round(attn_ms, 4) if attn_ms else None,
+                         "flops_per_launch": fl["global_attn_launch"], "traffic": None},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_threads)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

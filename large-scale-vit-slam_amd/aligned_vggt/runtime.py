@@ -1,0 +1,85 @@
+"""Host-side runtime for the HIP hot path: packed-weight cache and device
+workspaces.
+
+* Weights stay fp32 ``nn.Parameter``s with the reference module-tree names
+  (state-dict compatible, featureAligned_vggt.py:16-32); the bf16 operand
+  copies the MFMA kernels read are derived lazily and re-derived whenever the
+  parameter changes (tracked by ``_version`` / data pointer).
+* Activations live in per-device workspaces sized for the largest chunk seen
+  (288 GB of HBM per MI355X: buffers are kept, never freed per chunk -- the
+  reference instead calls ``torch.cuda.empty_cache()`` every chunk,
+  featureAligned_vggt.py:82).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+
+def _pkey(*ts):
+    return tuple((t.data_ptr(), t._version, t.device) if t is not None else None for t in ts)
+
+
+def pack_linear(lin: nn.Linear, k_pad: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(W bf16 [N, K(+pad)], bias rounded through bf16 as fp32 [N]).
+
+    Under the reference's bf16-mixed autocast nn.Linear casts weight AND bias
+    to bf16; the rounded bias is kept in fp32 for the epilogue add."""
+    w, b = lin.weight, lin.bias
+    key = _pkey(w, b) + (k_pad,)
+    c = lin.__dict__.get("_mi355x_pack")
+    if c is None or c[0] != key:
+        wq = w.detach().reshape(w.shape[0], -1).to(torch.bfloat16)
+        if k_pad:
+            wq = torch.nn.functional.pad(wq, (0, k_pad))
+        bq = (b.detach().to(torch.bfloat16).float() if b is not None
+              else torch.zeros(w.shape[0], device=w.device, dtype=torch.float32))
+        c = (key, wq.contiguous(), bq.contiguous())
+        lin.__dict__["_mi355x_pack"] = c
+    return c[1], c[2]
+
+
+def f32_param(mod: nn.Module, name: str, fill: Optional[float] = None, n: int = 0) -> torch.Tensor:
+    """fp32 contiguous view of a parameter (or a cached constant vector)."""
+    p = getattr(mod, name, None)
+    if p is None:
+        key = ("_mi355x_const", name, fill, n)
+        c = mod.__dict__.get(key[0] + name)
+        dev = next(mod.parameters()).device
+        if c is None or c.device != dev or c.numel() != n:
+            c = torch.full((n,), fill, device=dev, dtype=torch.float32)
+            mod.__dict__[key[0] + name] = c
+        return c
+    return p.detach().float().contiguous() if p.dtype != torch.float32 or not p.is_contiguous() else p.detach()
+
+
+class Workspace:
+    """Named, grow-only device buffers (one set per device)."""
+
+    _per_device: Dict[torch.device, "Workspace"] = {}
+
+    def __init__(self, device):
+        self.device = device
+        self.bufs: Dict[str, torch.Tensor] = {}
+
+    @classmethod
+    def get(cls, device) -> "Workspace":
+        device = torch.device(device)
+        ws = cls._per_device.get(device)
+        if ws is None:
+            ws = cls._per_device[device] = Workspace(device)
+        return ws
+
+    def buf(self, name: str, rows: int, cols: int, dtype=torch.float32) -> torch.Tensor:
+        t = self.bufs.get(name)
+        need = rows * cols
+        if t is None or t.dtype != dtype or t.numel() < need:
+            t = torch.zeros(need, device=self.device, dtype=dtype)
+            self.bufs[name] = t
+        return t[:need].view(rows, cols)
+
+
+def round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m

@@ -1,0 +1,40 @@
+"""Deterministic random-init weights and synthetic inputs (BASELINE.json
+configs use random-init weights and synthetic frames; no checkpoint or dataset
+is available offline -- SURVEY.md §8d).
+
+Every parameter draws from its own CPU ``torch.Generator`` seeded by
+``crc32(name) ^ seed``, so a module tree gets identical weights on any device
+and in any construction order.
+"""
+from __future__ import annotations
+
+import zlib
+
+import torch
+import torch.nn as nn
+
+# parameters whose constructor init is the reference's and is kept as is
+_KEEP = ("gamma", "camera_token", "register_token", "register_tokens", "cls_token", "mask_token",
+         "per_frame_alignment_token", "memory_token", "alpha", "empty_pose_tokens", "gate_mlp.2.")
+
+
+@torch.no_grad()
+def synthetic_init_(model: nn.Module, seed: int = 0, std: float = 0.02) -> nn.Module:
+    for name, p in model.named_parameters():
+        if any(k in name for k in _KEEP):
+            continue
+        g = torch.Generator().manual_seed((zlib.crc32(name.encode()) ^ seed) & 0x7FFFFFFF)
+        r = torch.randn(p.shape, generator=g, dtype=torch.float32)
+        is_norm_w = p.dim() == 1 and name.endswith("weight") and "norm" in name.split(".")[-2]
+        if is_norm_w:
+            v = 1.0 + std * r
+        else:
+            v = std * r
+        p.copy_(v.to(p.device, p.dtype))
+    return model
+
+
+def synthetic_images(B: int, S: int, H: int, W: int, seed: int = 1234, device="cpu") -> torch.Tensor:
+    """Uniform [0, 1) frames (B,S,3,H,W), generator seed 1234."""
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(B, S, 3, H, W, generator=g).to(device)

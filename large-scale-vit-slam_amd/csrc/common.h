@@ -1,0 +1,55 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of the VGGT hot path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/vggt_mi355x.h"
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef uint16_t bf16_t;  // raw bf16 bits in global memory
+
+#define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+// Round-to-nearest-even fp32 -> bf16 (finite inputs; NaN stays NaN via the
+// hardware convert path the compiler emits for __bf16 casts).
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+__device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+__device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
+
+// pack two floats into a dword of 2 bf16 (lo, hi)
+__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// XCD-aware bijective remap of a linear block id (cdna_hip_programming.md §5
+// "XCD swizzle must be bijective"): consecutive logical tiles land on the
+// same XCD (blocks b and b+8 share one), so tiles that share an operand panel
+// hit the same L2.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+#define HIP_LAUNCH_CHECK()                         \
+  do {                                             \
+    hipError_t e_ = hipGetLastError();             \
+    if (e_ != hipSuccess) return VGGT_ERR_HIP;     \
+  } while (0)

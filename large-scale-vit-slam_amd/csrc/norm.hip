@@ -1,0 +1,239 @@
+// Row LayerNorm and per-head QK-norm + RoPE (include/vggt_mi355x.h:
+// vggt_layernorm, vggt_headnorm_rope).  HBM-bound: one wave per row, 16-B
+// vectorised loads/stores, fp32 two-pass statistics in registers.
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- LayerNorm
+// NV = C / 256 float4 per lane (C = 256 * NV).
+template <int NV, bool IN_BF16, bool OUT_BF16>
+__global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__ x, int64_t ldx,
+                                                        const float* __restrict__ w, const float* __restrict__ b,
+                                                        float eps, int M, void* __restrict__ y, int64_t ldy) {
+  constexpr int C = NV * 256;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float v[NV][4];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = i * 256 + lane * 4;
+    if constexpr (IN_BF16) {
+      const uint2 u = *(const uint2*)((const bf16_t*)x + (int64_t)row * ldx + c);
+      v[i][0] = bf2f(u.x & 0xffff);
+      v[i][1] = bf2f(u.x >> 16);
+      v[i][2] = bf2f(u.y & 0xffff);
+      v[i][3] = bf2f(u.y >> 16);
+    } else {
+      const f32x4 u = *(const f32x4*)((const float*)x + (int64_t)row * ldx + c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[i][j] = u[j];
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += v[i][j];
+  const float mean = wave_sum(s) * (1.f / C);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float d = v[i][j] - mean;
+      q += d * d;
+    }
+  const float rstd = rsqrtf(wave_sum(q) * (1.f / C) + eps);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = i * 256 + lane * 4;
+    float o[4];
+    if (w) {
+      const f32x4 wv = *(const f32x4*)(w + c);
+      const f32x4 bv = b ? *(const f32x4*)(b + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd * wv[j] + bv[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd;
+    }
+    if constexpr (OUT_BF16) {
+      uint2 u;
+      u.x = pack_bf2(o[0], o[1]);
+      u.y = pack_bf2(o[2], o[3]);
+      *(uint2*)((bf16_t*)y + (int64_t)row * ldy + c) = u;
+    } else {
+      *(f32x4*)((float*)y + (int64_t)row * ldy + c) = f32x4{o[0], o[1], o[2], o[3]};
+    }
+  }
+}
+
+template <int NV>
+int launch_ln(const void* x, int in_bf, int64_t ldx, const float* w, const float* b, float eps, int M, void* y,
+              int out_bf, int64_t ldy, hipStream_t s) {
+  const int grid = (M + 3) / 4;
+  if (in_bf && out_bf) layernorm_kernel<NV, true, true><<<grid, 256, 0, s>>>(x, ldx, w, b, eps, M, y, ldy);
+  else if (in_bf) layernorm_kernel<NV, true, false><<<grid, 256, 0, s>>>(x, ldx, w, b, eps, M, y, ldy);
+  else if (out_bf) layernorm_kernel<NV, false, true><<<grid, 256, 0, s>>>(x, ldx, w, b, eps, M, y, ldy);
+  else layernorm_kernel<NV, false, false><<<grid, 256, 0, s>>>(x, ldx, w, b, eps, M, y, ldy);
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+// ------------------------------------------------- per-head norm + RoPE
+// One wave per row; each lane owns 8 consecutive values (one 16-B chunk) of
+// a head; LPH = D/8 lanes per head, heads processed 64/LPH at a time.
+template <int D, int MODE>
+__global__ __launch_bounds__(256) void headnorm_rope_kernel(bf16_t* __restrict__ buf, int64_t ld, int col_off, int M,
+                                                            int H, const float* __restrict__ w,
+                                                            const float* __restrict__ b, float eps,
+                                                            const int32_t* __restrict__ pos, int period,
+                                                            const float* __restrict__ cs, const float* __restrict__ sn,
+                                                            int tab_len) {
+  constexpr int LPH = D / 8;
+  constexpr int HPP = 64 / LPH;  // heads per pass
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int sub = lane % LPH;  // chunk index within the head
+  const int e0 = sub * 8;      // first element within the head
+  int p0 = 0, p1 = 0;
+  if constexpr (MODE == VGGT_ROPE_2D) {
+    const int pr = row % period;
+    p0 = min(max(pos[2 * pr], 0), tab_len - 1);
+    p1 = min(max(pos[2 * pr + 1], 0), tab_len - 1);
+  } else if constexpr (MODE == VGGT_ROPE_1D) {
+    p0 = min(max(pos[row % period], 0), tab_len - 1);
+  }
+  float wv[8], bv[8];
+  if (w) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      wv[j] = w[e0 + j];
+      bv[j] = b ? b[e0 + j] : 0.f;
+    }
+  }
+  for (int h0 = 0; h0 < H; h0 += HPP) {
+    const int h = h0 + lane / LPH;
+    const bool act = h < H;
+    bf16_t* p = buf + (int64_t)row * ld + col_off + (act ? h : 0) * D + e0;
+    float x[8];
+    {
+      const uint4 u = *(const uint4*)p;
+      const uint32_t uu[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x[2 * j] = bf2f(uu[j] & 0xffff);
+        x[2 * j + 1] = bf2f(uu[j] >> 16);
+      }
+    }
+    if (w) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += x[j];
+#pragma unroll
+      for (int o = 1; o < LPH; o <<= 1) s += __shfl_xor(s, o, 64);
+      const float mean = s * (1.f / D);
+      float q = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = x[j] - mean;
+        q += d * d;
+      }
+#pragma unroll
+      for (int o = 1; o < LPH; o <<= 1) q += __shfl_xor(q, o, 64);
+      const float rstd = rsqrtf(q * (1.f / D) + eps);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = (x[j] - mean) * rstd * wv[j] + bv[j];
+    }
+    if constexpr (MODE != VGGT_ROPE_NONE) {
+      // rotate_half partner lives RD/2 elements away = (RD/16) lanes away
+      constexpr int RD = (MODE == VGGT_ROPE_2D) ? D / 2 : D;
+      constexpr int PL = RD / 16;  // partner lane distance
+      const int er = e0 % RD;      // element index inside the rotated block
+      const int pp = (MODE == VGGT_ROPE_2D && e0 >= D / 2) ? p1 : p0;
+      const bool first = er < RD / 2;
+      float y[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float partner = __shfl_xor(x[j], PL, 64);
+        const float rot = first ? -partner : partner;
+        y[j] = x[j] * cs[pp * RD + er + j] + rot * sn[pp * RD + er + j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = y[j];
+    }
+    if (act) {
+      uint4 u;
+      u.x = pack_bf2(x[0], x[1]);
+      u.y = pack_bf2(x[2], x[3]);
+      u.z = pack_bf2(x[4], x[5]);
+      u.w = pack_bf2(x[6], x[7]);
+      *(uint4*)p = u;
+    }
+  }
+}
+
+template <int D>
+int launch_hnr(bf16_t* buf, int64_t ld, int col_off, int M, int H, const float* w, const float* b, float eps, int mode,
+               const int32_t* pos, int period, const float* cs, const float* sn, int tab_len, hipStream_t s) {
+  const int grid = (M + 3) / 4;
+  switch (mode) {
+    case VGGT_ROPE_NONE:
+      headnorm_rope_kernel<D, VGGT_ROPE_NONE><<<grid, 256, 0, s>>>(buf, ld, col_off, M, H, w, b, eps, pos, period, cs,
+                                                                  sn, tab_len);
+      break;
+    case VGGT_ROPE_2D:
+      headnorm_rope_kernel<D, VGGT_ROPE_2D><<<grid, 256, 0, s>>>(buf, ld, col_off, M, H, w, b, eps, pos, period, cs, sn,
+                                                                tab_len);
+      break;
+    case VGGT_ROPE_1D:
+      headnorm_rope_kernel<D, VGGT_ROPE_1D><<<grid, 256, 0, s>>>(buf, ld, col_off, M, H, w, b, eps, pos, period, cs, sn,
+                                                                tab_len);
+      break;
+    default: return VGGT_ERR_UNSUPPORTED;
+  }
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+}  // namespace
+
+extern "C" int vggt_layernorm(const void* x, int in_dtype, int64_t ldx, const float* w, const float* b, float eps,
+                              int M, int C, void* y, int out_dtype, int64_t ldy, void* stream) {
+  if (M <= 0) return M == 0 ? VGGT_OK : VGGT_ERR_SHAPE;
+  if (C % 256 || C > 4096 || C <= 0) return VGGT_ERR_SHAPE;
+  if ((in_dtype != VGGT_DTYPE_F32 && in_dtype != VGGT_DTYPE_BF16) ||
+      (out_dtype != VGGT_DTYPE_F32 && out_dtype != VGGT_DTYPE_BF16))
+    return VGGT_ERR_UNSUPPORTED;
+  if ((ldx % 4) || (ldy % 4) || ((uintptr_t)x % 8) || ((uintptr_t)y % 8)) return VGGT_ERR_ALIGN;
+  if (!in_dtype && ((uintptr_t)x % 16)) return VGGT_ERR_ALIGN;
+  if (!out_dtype && ((uintptr_t)y % 16)) return VGGT_ERR_ALIGN;
+  hipStream_t s = (hipStream_t)stream;
+  const int ib = in_dtype == VGGT_DTYPE_BF16, ob = out_dtype == VGGT_DTYPE_BF16;
+  switch (C / 256) {
+    case 1: return launch_ln<1>(x, ib, ldx, w, b, eps, M, y, ob, ldy, s);
+    case 2: return launch_ln<2>(x, ib, ldx, w, b, eps, M, y, ob, ldy, s);
+    case 3: return launch_ln<3>(x, ib, ldx, w, b, eps, M, y, ob, ldy, s);
+    case 4: return launch_ln<4>(x, ib, ldx, w, b, eps, M, y, ob, ldy, s);
+    case 8: return launch_ln<8>(x, ib, ldx, w, b, eps, M, y, ob, ldy, s);
+    case 16: return launch_ln<16>(x, ib, ldx, w, b, eps, M, y, ob, ldy, s);
+    default: return VGGT_ERR_SHAPE;
+  }
+}
+
+extern "C" int vggt_headnorm_rope(void* buf, int64_t ld, int col_off, int M, int H, int D, const float* w,
+                                  const float* b, float eps, int rope_mode, const int32_t* pos, int period,
+                                  const float* cos_tab, const float* sin_tab, int tab_len, void* stream) {
+  if (M <= 0) return M == 0 ? VGGT_OK : VGGT_ERR_SHAPE;
+  if (H <= 0 || (D != 64 && D != 128)) return VGGT_ERR_SHAPE;
+  if ((ld % 8) || (col_off % 8) || ((uintptr_t)buf % 16)) return VGGT_ERR_ALIGN;
+  if (rope_mode != VGGT_ROPE_NONE && (!pos || !cos_tab || !sin_tab || period <= 0 || tab_len <= 0))
+    return VGGT_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  if (D == 64) return launch_hnr<64>((bf16_t*)buf, ld, col_off, M, H, w, b, eps, rope_mode, pos, period, cos_tab, sin_tab,
+                                     tab_len, s);
+  return launch_hnr<128>((bf16_t*)buf, ld, col_off, M, H, w, b, eps, rope_mode, pos, period, cos_tab, sin_tab, tab_len, s);
+}

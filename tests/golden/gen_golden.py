@@ -1,0 +1,228 @@
+"""Generate golden fixtures from the reference's own code (run in the build
+container only; /root/reference does not exist on the GPU box).
+
+What it runs:
+  * ``aligned_vggt.layers.rope.RotaryPositionEmbedding`` and
+    ``aligned_vggt.layers.gated_update.GatedUpdate`` imported directly from
+    /root/reference (both import standalone);
+  * pure-torch/numpy functions pulled out of modules whose module-level
+    ``vggt`` imports fail, by parsing the file with ``ast`` and executing only
+    those ``def``s (no stand-in for the missing ``vggt`` package is written);
+  * ``transformers`` Dinov2WithRegistersModel (third-party, in-container) as an
+    independent pin of the DINOv2 stage.
+
+Outputs are data only (inputs + expected outputs) in ``tests/golden/*.npz``.
+Usage:  python tests/golden/gen_golden.py [--ref /root/reference]
+"""
+from __future__ import annotations
+
+import argparse
+import ast
+import os
+import random
+import sys
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def extract(ref: str, relpath: str, names):
+    """Exec only the named top-level functions of a reference file."""
+    src = open(os.path.join(ref, relpath)).read()
+    tree = ast.parse(src)
+    keep = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name in names]
+    missing = set(names) - {n.name for n in keep}
+    assert not missing, missing
+    mod = ast.Module(body=keep, type_ignores=[])
+    g = {"torch": torch, "np": np, "F": F, "Optional": Optional, "Tuple": Tuple, "random": random,
+         "__name__": "golden_extract"}
+    exec(compile(mod, relpath, "exec"), g)
+    return {n: g[n] for n in names}
+
+
+def save(name, **arrays):
+    out = {}
+    for k, v in arrays.items():
+        if isinstance(v, torch.Tensor):
+            v = v.detach().cpu().numpy()
+        out[k] = np.asarray(v)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print("wrote", name, {k: v.shape for k, v in out.items()})
+
+
+def gen_rope(ref):
+    sys.path.insert(0, ref)
+    from aligned_vggt.layers.rope import RotaryPositionEmbedding  # reference module
+    g = torch.Generator().manual_seed(11)
+    rope = RotaryPositionEmbedding(frequency=100.0)
+    cases = {}
+    for ci, (B, H, N, D, maxp) in enumerate([(3, 2, 5, 16, 9), (2, 8, 16, 128, 20), (4, 8, 24, 64, 40)]):
+        x = torch.randn(B, H, N, D, generator=g)
+        pos = torch.randint(0, maxp, (B, N), generator=g)
+        y = rope(x, pos)
+        cases[f"x{ci}"] = x
+        cases[f"pos{ci}"] = pos
+        cases[f"y{ci}"] = y
+    save("rope1d", **cases)
+
+
+def gen_gated_update(ref):
+    sys.path.insert(0, ref)
+    from aligned_vggt.layers.gated_update import GatedUpdate  # reference module
+    torch.manual_seed(5)
+    save("gated_update_nparams", d512_n8=np.array(sum(p.numel() for p in GatedUpdate(512, 8).parameters())))
+    for D, N, tag in [(64, 8, "d64"), (32, 4, "d32")]:
+        m = GatedUpdate(D, N).eval()
+        mem = F.normalize(torch.randn(2, N, D), dim=-1)
+        upd = torch.randn(2, 1, D) * 3.0
+        with torch.no_grad():
+            out = m(mem, upd)
+        sd = {"p." + k: v for k, v in m.state_dict().items()}
+        save("gated_update_" + tag, memory=mem, update=upd, out=out,
+             nparams=np.array(sum(p.numel() for p in m.parameters())), **sd)
+
+
+def gen_chunks(ref):
+    fn = extract(ref, "aligned_vggt/utils/data.py", ["generate_chunks"])["generate_chunks"]
+    rows = []
+    for n in [1, 4, 5, 8, 14, 16, 17, 20, 33, 64, 100, 512]:
+        for w in [2, 5, 8, 16, 75]:
+            for ov in [0, 1, 2, 4, 30]:
+                if ov >= w:
+                    continue
+                for ci, c in enumerate(fn(n, "chunk_overlap", w, ov)):
+                    for f in c:
+                        rows.append((n, w, ov, ci, f))
+    save("generate_chunks", rows=np.array(rows, dtype=np.int64))
+
+
+def gen_geometry(ref):
+    fns = extract(ref, "aligned_vggt/utils/geometry.py", ["averagePoseEncodings"])
+    g = torch.Generator().manual_seed(3)
+    enc = torch.randn(6, 4, 7, generator=g, dtype=torch.float64).float()
+    enc[..., 3:7] = F.normalize(enc[..., 3:7] * 0.1 + torch.tensor([0, 0, 0, 1.0]), dim=-1)
+    out = fns["averagePoseEncodings"](enc)
+    save("average_pose_encodings", enc=enc, out=out)
+
+
+def gen_alignment(ref):
+    fns = extract(ref, "aligned_vggt/utils/alignment.py",
+                  ["umeyama", "scale_lse_solver", "apply_sim3_alignment_on_point_maps", "apply_sim3_alignment_on_c2w"])
+    rng = np.random.default_rng(9)
+    x = rng.normal(size=(3, 50))
+    ang = 0.4
+    R = np.array([[np.cos(ang), -np.sin(ang), 0], [np.sin(ang), np.cos(ang), 0], [0, 0, 1.0]])
+    y = 1.7 * R @ x + np.array([[0.3], [-1.0], [2.0]]) + rng.normal(size=(3, 50)) * 1e-3
+    r, t, c = fns["umeyama"](x, y)
+    s = fns["scale_lse_solver"](x.reshape(-1), y.reshape(-1))
+    pm = torch.randn(2, 3, 4, 5, 3, dtype=torch.float32)
+    T = torch.eye(4).repeat(2, 1, 1)
+    T[:, :3, :3] = torch.tensor(R, dtype=torch.float32)
+    T[:, :3, 3] = torch.tensor([0.5, -0.2, 1.0])
+    sc = torch.tensor([1.5, 0.7])
+    pm_out = fns["apply_sim3_alignment_on_point_maps"](pm, T, sc)
+    poses = torch.eye(4).repeat(2, 3, 1, 1)
+    poses[..., :3, 3] = torch.randn(2, 3, 3)
+    c2w_out = fns["apply_sim3_alignment_on_c2w"](poses.clone(), T, sc)
+    save("alignment_utils", x=x, y=y, r=r, t=t, c=np.array(c), s=np.array(s), pm=pm, T=T, sc=sc, pm_out=pm_out,
+         poses=poses, c2w_out=c2w_out)
+
+
+def gen_irls(ref):
+    fns = extract(ref, "aligned_vggt/models/pointAligned_wrapped_vggt.py",
+                  ["weighted_umeyama_sim3", "irls_sim3_umeyama"])
+    g = torch.Generator().manual_seed(21)
+    src = torch.randn(2, 6, 8, 3, generator=g)
+    ang = 0.3
+    R = torch.tensor([[1, 0, 0], [0, np.cos(ang), -np.sin(ang)], [0, np.sin(ang), np.cos(ang)]], dtype=torch.float32)
+    dst = 0.8 * src @ R.T + torch.tensor([1.0, 2.0, -0.5])
+    dst = dst + 0.01 * torch.randn(dst.shape, generator=g)
+    dst[0, 0, :5] += 3.0  # outliers for the Huber weights
+    cs = 1 + torch.rand(2, 6, 8, generator=g) * 5
+    cd = 1 + torch.rand(2, 6, 8, generator=g) * 5
+    r, t, s = fns["irls_sim3_umeyama"](src, dst, cs, cd)
+    save("irls_sim3", src=src, dst=dst, conf_src=cs, conf_dst=cd, r=r, t=t, s=np.array(float(s)))
+
+
+def gen_small_fns(ref):
+    mr = extract(ref, "aligned_vggt/models/featureAligned_vggt.py", ["merge_results"])["merge_results"]
+    se = extract(ref, "aligned_vggt/heads/alignment_head.py", ["slice_expand_and_flatten"])["slice_expand_and_flatten"]
+    a = torch.arange(2 * 3 * 7, dtype=torch.float32).view(2, 3, 7)
+    b = -torch.arange(2 * 4 * 7, dtype=torch.float32).view(2, 4, 7)
+    tok = torch.randn(1, 2, 3, 5)
+    save("small_fns", a=a, b=b, merged0=mr(a, b, 0, 1), merged2=mr(a, b, 2, 1), tok=tok, sef=se(tok, 2, 4))
+
+
+def gen_dinov2():
+    """Independent third-party pin of the DINOv2 stage (ext)."""
+    from transformers import Dinov2WithRegistersConfig, Dinov2WithRegistersModel
+    cfg = Dinov2WithRegistersConfig(hidden_size=64, num_hidden_layers=2, num_attention_heads=4, intermediate_size=256,
+                                    image_size=56, patch_size=14, num_register_tokens=4, layerscale_value=1.0,
+                                    layer_norm_eps=1e-6, hidden_act="gelu", qkv_bias=True)
+    torch.manual_seed(2)
+    m = Dinov2WithRegistersModel(cfg).eval()
+    with torch.no_grad():
+        for prm in m.parameters():
+            prm.copy_(torch.randn_like(prm) * 0.05)
+        for blk in m.encoder.layer:
+            blk.layer_scale1.lambda1.fill_(1.0)
+            blk.layer_scale2.lambda1.fill_(1.0)
+    # Map to VGGT/DINOv2 (aggregator.patch_embed.*) names.
+    hf = m.state_dict()
+    sd = {
+        "cls_token": hf["embeddings.cls_token"],
+        "pos_embed": hf["embeddings.position_embeddings"],
+        "register_tokens": hf["embeddings.register_tokens"],
+        "patch_embed.proj.weight": hf["embeddings.patch_embeddings.projection.weight"],
+        "patch_embed.proj.bias": hf["embeddings.patch_embeddings.projection.bias"],
+        "norm.weight": hf["layernorm.weight"],
+        "norm.bias": hf["layernorm.bias"],
+    }
+    for i in range(cfg.num_hidden_layers):
+        h = f"encoder.layer.{i}."
+        o = f"blocks.{i}."
+        sd[o + "norm1.weight"] = hf[h + "norm1.weight"]
+        sd[o + "norm1.bias"] = hf[h + "norm1.bias"]
+        sd[o + "attn.qkv.weight"] = torch.cat([hf[h + f"attention.attention.{n}.weight"] for n in ("query", "key", "value")])
+        sd[o + "attn.qkv.bias"] = torch.cat([hf[h + f"attention.attention.{n}.bias"] for n in ("query", "key", "value")])
+        sd[o + "attn.proj.weight"] = hf[h + "attention.output.dense.weight"]
+        sd[o + "attn.proj.bias"] = hf[h + "attention.output.dense.bias"]
+        sd[o + "ls1.gamma"] = hf[h + "layer_scale1.lambda1"]
+        sd[o + "norm2.weight"] = hf[h + "norm2.weight"]
+        sd[o + "norm2.bias"] = hf[h + "norm2.bias"]
+        sd[o + "mlp.fc1.weight"] = hf[h + "mlp.fc1.weight"]
+        sd[o + "mlp.fc1.bias"] = hf[h + "mlp.fc1.bias"]
+        sd[o + "mlp.fc2.weight"] = hf[h + "mlp.fc2.weight"]
+        sd[o + "mlp.fc2.bias"] = hf[h + "mlp.fc2.bias"]
+        sd[o + "ls2.gamma"] = hf[h + "layer_scale2.lambda1"]
+    g = torch.Generator().manual_seed(4)
+    outs = {}
+    for tag, (H, W) in {"sq": (56, 56), "rect": (28, 56)}.items():
+        img = torch.randn(2, 3, H, W, generator=g)
+        with torch.no_grad():
+            last = m(pixel_values=img).last_hidden_state  # already final-layernormed
+        outs[f"img_{tag}"] = img
+        outs[f"patch_{tag}"] = last[:, 1 + cfg.num_register_tokens:]
+    save("dinov2_hf", **outs, **{"sd." + k: v for k, v in sd.items()})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    a = ap.parse_args()
+    gen_rope(a.ref)
+    gen_gated_update(a.ref)
+    gen_chunks(a.ref)
+    gen_geometry(a.ref)
+    gen_alignment(a.ref)
+    gen_irls(a.ref)
+    gen_small_fns(a.ref)
+    gen_dinov2()
+
+
+if __name__ == "__main__":
+    main()

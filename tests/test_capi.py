@@ -1,0 +1,45 @@
+"""CPU-side checks of the C-ABI boundary: the built library loads and exports
+every function declared in include/*.h (no compute calls without a GPU)."""
+import ctypes
+import glob
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b(vggt_[a-z0-9_]+)\s*\(", src))
+    return names
+
+
+def test_header_declares_entry_points():
+    names = _declared()
+    assert {"vggt_gemm_bf16", "vggt_attention_fwd", "vggt_layernorm", "vggt_headnorm_rope"} <= names
+
+
+def test_library_exports_every_declared_symbol():
+    from aligned_vggt import _native
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("library not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    missing = [n for n in sorted(_declared()) if not hasattr(lib, n)]
+    assert not missing, missing
+    assert _native.version().startswith("vggt_mi355x")
+    # every binding signature refers to a declared symbol
+    assert set(_native._SIGS) <= _declared()
+
+
+def test_product_refuses_cpu_tensors():
+    import torch
+    from aligned_vggt import _native
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("library not built")
+    a = torch.zeros(128, 64, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="HIP devices only"):
+        _native.gemm_bf16(a, a, torch.zeros(128), torch.zeros(128, 128, dtype=torch.bfloat16), 0)

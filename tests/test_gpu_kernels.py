@@ -1,0 +1,175 @@
+"""GPU parity of the individual HIP kernels (through the C ABI) against plain
+PyTorch fp32 references of the same op / the CPU oracle's functions."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from oracle import vggt_oracle as O  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def N():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from aligned_vggt import _native
+    _native.lib()
+    return _native
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("M,Nn,K", [(128, 128, 64), (300, 256, 192), (1374, 1024, 1024), (77, 3072, 640)])
+@pytest.mark.parametrize("epi", [0, 1, 2, 3])
+def test_gemm_epilogues(N, M, Nn, K, epi):
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + epi)
+    a = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    # asymmetric operand (catches transposed C writes)
+    w = (torch.randn(Nn, K, device="cuda", generator=g) + torch.arange(Nn, device="cuda")[:, None] * 1e-3).to(torch.bfloat16)
+    b = torch.randn(Nn, device="cuda", generator=g).to(torch.bfloat16).float()
+    ref = a.float() @ w.float().t() + b
+    refb = ref.to(torch.bfloat16).float()
+    if epi == N.EPI_BF16:
+        out = torch.empty(M, Nn, device="cuda", dtype=torch.bfloat16)
+        N.gemm_bf16(a, w, b, out, epi)
+        assert _rel(out, refb) < 4e-3
+    elif epi == N.EPI_GELU_BF16:
+        out = torch.empty(M, Nn, device="cuda", dtype=torch.bfloat16)
+        N.gemm_bf16(a, w, b, out, epi)
+        assert _rel(out, F.gelu(refb)) < 6e-3
+    elif epi == N.EPI_RESID_F32:
+        x0 = torch.randn(M, Nn, device="cuda", generator=g)
+        gam = torch.rand(Nn, device="cuda", generator=g)
+        x = x0.clone()
+        o2 = torch.zeros(M, 2 * Nn, device="cuda")
+        N.gemm_bf16(a, w, b, x, epi, gamma=gam, out2=o2[:, Nn:])
+        r = x0 + gam * refb
+        assert _rel(x, r) < 4e-3
+        torch.testing.assert_close(o2[:, Nn:], x)
+        assert o2[:, :Nn].abs().max().item() == 0
+    else:
+        out = torch.empty(M, Nn, device="cuda")
+        N.gemm_bf16(a, w, b, out, epi)
+        assert _rel(out, refb) < 4e-3
+
+
+def test_gemm_rejects_bad_shapes(N):
+    a = torch.zeros(64, 100, device="cuda", dtype=torch.bfloat16)
+    w = torch.zeros(128, 100, device="cuda", dtype=torch.bfloat16)
+    b = torch.zeros(128, device="cuda")
+    with pytest.raises(RuntimeError, match="shape"):
+        N.gemm_bf16(a, w, b, torch.empty(64, 128, device="cuda", dtype=torch.bfloat16), 0)
+
+
+@pytest.mark.parametrize("C", [512, 1024, 2048])
+@pytest.mark.parametrize("ib,ob", [(False, True), (False, False), (True, False)])
+def test_layernorm(N, C, ib, ob):
+    x = torch.randn(301, C, device="cuda") * 3 + 1
+    if ib:
+        x = x.to(torch.bfloat16)
+    w = torch.randn(C, device="cuda")
+    b = torch.randn(C, device="cuda")
+    out = torch.empty(301, C, device="cuda", dtype=torch.bfloat16 if ob else torch.float32)
+    N.layernorm(x, w, b, 1e-6, out)
+    ref = F.layer_norm(x.float(), (C,), w, b, 1e-6)
+    assert _rel(out, ref) < (4e-3 if ob else 1e-5)
+
+
+@pytest.mark.parametrize("D,mode", [(64, 1), (128, 1), (64, 0), (128, 2), (64, 2)])
+def test_headnorm_rope(N, D, mode):
+    H = 1024 // D
+    M = 3 * 21
+    g = torch.Generator().manual_seed(D + mode)
+    qkv = (torch.randn(M, 3 * 1024, generator=g) * 2).to(torch.bfloat16)
+    w = torch.randn(D, generator=g)
+    b = torch.randn(D, generator=g)
+    if mode == 1:
+        pos = O.position_grid(1, 4, 4, 5)[0]
+        period = pos.shape[0]
+        from aligned_vggt.backbone.layers import RopeTables
+        rt = RopeTables(pos, D, 100.0, "cuda")
+    elif mode == 2:
+        pos = torch.randint(0, 30, (7,), generator=g)
+        period = 7
+        from aligned_vggt.backbone.layers import RopeTables
+        rt = RopeTables(pos, D, 100.0, "cuda", mode=2)
+    buf = qkv.cuda()
+    N.headnorm_rope(buf, 1024, H, D, w.cuda(), b.cuda(), 1e-5, mode, rt.pos if mode else None, period if mode else 1,
+                    rt.cos if mode else None, rt.sin if mode else None)
+    # oracle: (B=1, heads, N, D)
+    k = qkv[:, 1024:2048].float().reshape(M, H, D).permute(1, 0, 2)[None]
+    k = O.layer_norm(k, w, b, 1e-5)
+    if mode == 1:
+        pfull = pos.repeat(M // period, 1)[None]
+        k = O.rope2d(k, pfull)
+    elif mode == 2:
+        pfull = pos.repeat(M // period)[None]
+        k = O.rope1d(k, pfull)
+    ref = k[0].permute(1, 0, 2).reshape(M, 1024)
+    got = buf[:, 1024:2048].float().cpu()
+    assert _rel(got, ref) < 4e-3
+    # q/v columns untouched
+    assert torch.equal(buf[:, 2048:].cpu(), qkv[:, 2048:])
+    assert torch.equal(buf[:, :1024].cpu(), qkv[:, :1024])
+
+
+def _ref_attn(q, k, v, scale):
+    s = (q.float() @ k.float().transpose(-1, -2)) * scale
+    return torch.softmax(s, -1) @ v.float()
+
+
+@pytest.mark.parametrize("D,H,batch,n", [(64, 16, 3, 21), (64, 16, 2, 1374), (128, 8, 2, 1375), (64, 2, 1, 4100),
+                                         (128, 2, 1, 64), (64, 1, 1, 1)])
+def test_attention_vs_torch(N, D, H, batch, n):
+    C = H * D
+    g = torch.Generator(device="cuda").manual_seed(n + D)
+    qkv = (torch.randn(batch * n, 3 * C, device="cuda", generator=g) * 1.5).to(torch.bfloat16)
+    o = torch.zeros(batch * n, C, device="cuda", dtype=torch.bfloat16)
+    N.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, batch, H, n, n, D, n, n, n)
+    t = qkv.float().view(batch, n, 3, H, D).permute(2, 0, 3, 1, 4)
+    ref = _ref_attn(t[0], t[1], t[2], D ** -0.5).permute(0, 2, 1, 3).reshape(batch * n, C)
+    assert _rel(o, ref) < 1e-2, _rel(o, ref)
+
+
+def test_attention_global_shape_rows(N):
+    """Full BASELINE global-attention shape (1 x 16 heads x 21984 x 64):
+    spot-check 256 query rows of every head against an fp32 reference."""
+    n, H, D = 16 * 1374, 16, 64
+    C = H * D
+    g = torch.Generator(device="cuda").manual_seed(0)
+    qkv = torch.randn(n, 3 * C, device="cuda", generator=g).to(torch.bfloat16)
+    o = torch.empty(n, C, device="cuda", dtype=torch.bfloat16)
+    N.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, 1, H, n, n, D, n, n, n)
+    rows = torch.randperm(n, generator=torch.Generator().manual_seed(1))[:256].cuda()
+    q = qkv[rows, :C].float().view(-1, H, D).transpose(0, 1)
+    k = qkv[:, C:2 * C].float().view(n, H, D).transpose(0, 1)
+    v = qkv[:, 2 * C:].float().view(n, H, D).transpose(0, 1)
+    ref = _ref_attn(q, k, v, D ** -0.5).transpose(0, 1).reshape(-1, C)
+    assert _rel(o[rows], ref) < 1e-2
+
+
+def test_attention_online_softmax_rescale(N):
+    """Force the running max to jump late (rule 26): one key with a huge score
+    in the last tile for some rows."""
+    n, H, D = 700, 2, 64
+    C = H * D
+    q = torch.randn(n, C, device="cuda") * 0.1
+    k = torch.randn(n, C, device="cuda") * 0.1
+    v = torch.randn(n, C, device="cuda")
+    k[650] = 3.0
+    q[:50] = 3.0
+    qkv = torch.cat([q, k, v], 1).to(torch.bfloat16)
+    o = torch.empty(n, C, device="cuda", dtype=torch.bfloat16)
+    N.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, 1, H, n, n, D, n, n, n)
+    t = qkv.float().view(1, n, 3, H, D).permute(2, 0, 3, 1, 4)
+    ref = _ref_attn(t[0], t[1], t[2], D ** -0.5).permute(0, 2, 1, 3).reshape(n, C)
+    assert _rel(o, ref) < 1e-2
