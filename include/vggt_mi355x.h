@@ -123,6 +123,79 @@ int vggt_special_tokens(float* x, int64_t ldx, int F, int S, int P, int n, int C
 /* Strided 2-D copy of f32 rows: dst[r*ldd + c] = src[r*lds + c], r < rows, c < cols. */
 int vggt_copy_rows_f32(const float* src, int64_t lds, float* dst, int64_t ldd, int rows, int cols, void* stream);
 
+/*
+ * Row-remapped LayerNorm: logical row r (< M) = group g = r / group, i = r % group,
+ * reads x row g*x_group_stride + x_row_offset + i and writes y row
+ * g*y_group_stride + y_row_offset + i.  Used to skip/insert per-frame special
+ * tokens without copies: DPT patch-token norm (dpt_head, ext, via
+ * featureAligned_vggt.py:166) and AlignmentHead.token_norm writing after the
+ * per-frame alignment token (alignment_head.py:247,269-270).
+ */
+int vggt_layernorm_grouped(const void* x, int in_dtype, int64_t ldx, const float* w, const float* b, float eps, int M,
+                           int C, void* y, int out_dtype, int64_t ldy, int group, int x_group_stride,
+                           int x_row_offset, int y_group_stride, int y_row_offset, void* stream);
+
+/*
+ * Skinny fp32 linear layer (weight-streaming, small M), exact-f32 MFMA:
+ *   out[M,N] = epi( act_in(A)[M,K] . W[N,K]^T + bias )
+ * act_in: 0 none, 1 SiLU.  epi: VGGT_EPI_F32 (plain), VGGT_EPI_GELU_BF16 (GELU,
+ * f32 out here), VGGT_EPI_RESID_F32 (out += gamma * v; out is the residual).
+ * Replaces the fp32 nn.Linear calls of the camera head (camera_head, ext:
+ * embed_pose, poseLN_modulation, trunk Blocks, pose_branch), the alignment
+ * decoder (alignment_head.py:463,475,534-538, cross blocks, gated_update.py:22-36).
+ */
+int vggt_linear_f32(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, int M, int N, int K,
+                    int act_in, int epi, float* out, int64_t ldo, const float* gamma, void* stream);
+
+/*
+ * Small-window attention (nk <= 128, D <= 256), one wave per (batch, head),
+ * f32 softmax; dtype VGGT_DTYPE_BF16 or VGGT_DTYPE_F32 for all of q/k/v/o.
+ * Layout as vggt_attention_fwd (v shares k's batch stride).  Replaces the SDPA
+ * of CrossAttention (cross_attention.py:64-73) in the temporal blocks (S
+ * queries x T keys per spatial token, alignment_head.py:368-390) and the
+ * decoder (alignment_head.py:494-530), and the camera-head trunk attention.
+ */
+int vggt_attention_small(const void* q, int64_t ldq, int64_t q_bstride, const void* k, int64_t ldk, int64_t k_bstride,
+                         const void* v, int64_t ldv, void* o, int64_t ldo, int64_t o_bstride, int dtype, int batch,
+                         int heads, int nq, int nk, int D, float scale, void* stream);
+
+/* fp32 variant of vggt_headnorm_rope (decoder / camera head run in fp32). */
+int vggt_headnorm_rope_f32(float* buf, int64_t ld, int col_off, int M, int H, int D, const float* w, const float* b,
+                           float eps, int rope_mode, const int32_t* pos, int period, const float* cos_tab,
+                           const float* sin_tab, int tab_len, void* stream);
+
+/* y_bf16[r, c] = bf16(x_f32[r, c])  (autocast input cast of a Linear). */
+int vggt_cast_f32_bf16(const float* x, int64_t ldx, void* y, int64_t ldy, int rows, int cols, void* stream);
+
+/*
+ * fp32 NHWC implicit-GEMM convolution (exact-f32 MFMA), DPT head
+ * (dpt_head, ext; featureAligned_vggt.py:166,183):
+ *   y[p, co] = relu_out?( sum act(x) * W + bias ) [+ pos[p % (ho*wo), co]]
+ *              [+ (res1_relu ? relu(res1) : res1)[p, co]] [+ res2[p, co]]
+ * x: [nimg, hi, wi, ci] with pixel stride ldx; W: [roundup(co',64), kh*kw*ci]
+ * (K order ky, kx, ci; rows beyond co' zero-padded); ci % 32 == 0.
+ * shuffle = s > 0 turns a 1x1 GEMM with co' = s*s*co columns (column
+ * (dy*s+dx)*co + c) into a stride==kernel ConvTranspose2d pixel-shuffle store
+ * onto the [nimg, hi*s, wi*s, co] grid.
+ */
+int vggt_conv2d_f32(const float* x, int64_t ldx, int nimg, int hi, int wi, int ci, const float* w, const float* bias,
+                    int co, int kh, int kw, int stride, int pad, float* y, int64_t ldy, int relu_in, int relu_out,
+                    const float* res1, int64_t ldr1, int res1_relu, const float* res2, int64_t ldr2, const float* pos,
+                    int shuffle, void* stream);
+
+/* NHWC bilinear resize with align_corners=True (custom_interpolate, dpt_head ext), + optional pos table. */
+int vggt_upsample_bilinear_f32(const float* x, int nimg, int hi, int wi, int C, float* y, int ho, int wo,
+                               const float* pos, void* stream);
+
+/*
+ * DPT activate_head (ext): x [npix, ncl] NHWC with the confidence last;
+ * pts[p, j] = act(x[p, j]) * scale[p / pix_per_img]  (act 0 = exp, 1 = inv_log),
+ * conf[p] = 1 + exp(x[p, ncl-1]) (expp1).  scale may be NULL (depth *= chunk
+ * scale, featureAligned_vggt.py:171).
+ */
+int vggt_dpt_activate(const float* x, int64_t ldx, int64_t npix, int pix_per_img, int ncl, int act,
+                      const float* scale, float* pts, float* conf, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -35,6 +35,16 @@ _SIGS = {
     "vggt_dino_assemble": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp],
     "vggt_special_tokens": [_vp, _i64, _i, _i, _i, _i, _i, _vp, _vp],
     "vggt_copy_rows_f32": [_vp, _i64, _vp, _i64, _i, _i, _vp],
+    "vggt_layernorm_grouped": [_vp, _i, _i64, _vp, _vp, _f, _i, _i, _vp, _i, _i64, _i, _i, _i, _i, _i, _vp],
+    "vggt_linear_f32": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _i, _vp, _i64, _vp, _vp],
+    "vggt_attention_small": [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i64, _i, _i, _i, _i, _i, _i, _f,
+                             _vp],
+    "vggt_headnorm_rope_f32": [_vp, _i64, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _i, _vp, _vp, _i, _vp],
+    "vggt_cast_f32_bf16": [_vp, _i64, _vp, _i64, _i, _i, _vp],
+    "vggt_conv2d_f32": [_vp, _i64, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _i64, _i, _i, _vp, _i64, _i, _vp,
+                        _i64, _vp, _i, _vp],
+    "vggt_upsample_bilinear_f32": [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp],
+    "vggt_dpt_activate": [_vp, _i64, _i64, _i, _i, _i, _vp, _vp, _vp, _vp],
 }
 
 _lib = None
@@ -171,3 +181,88 @@ def copy_rows_f32(src: torch.Tensor, dst: torch.Tensor) -> None:
     _dev(src, "copy_rows_f32")
     rc = lib().vggt_copy_rows_f32(_p(src), _ld(src), _p(dst), _ld(dst), src.shape[0], src.shape[1], _stream())
     _check(rc, "vggt_copy_rows_f32")
+
+
+def _dt(t: torch.Tensor) -> int:
+    if t.dtype == torch.bfloat16:
+        return DTYPE_BF16
+    if t.dtype == torch.float32:
+        return DTYPE_F32
+    raise RuntimeError(f"unsupported dtype {t.dtype}")
+
+
+def layernorm_grouped(x: torch.Tensor, w, b, eps: float, out: torch.Tensor, M: int, C: int, group: int,
+                      x_gstride: int, x_off: int, y_gstride: int, y_off: int) -> None:
+    _dev(x, "layernorm_grouped")
+    rc = lib().vggt_layernorm_grouped(_p(x), _dt(x), _ld(x), _p(w), _p(b), float(eps), M, C, _p(out), _dt(out),
+                                      _ld(out), group, x_gstride, x_off, y_gstride, y_off, _stream())
+    _check(rc, "vggt_layernorm_grouped")
+
+
+def linear_f32(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], out: torch.Tensor, epi: int = EPI_F32,
+               act_in: int = 0, gamma: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _dev(a, "linear_f32")
+    M, K = a.shape
+    N_ = w.shape[0]
+    assert a.dtype == torch.float32 and w.dtype == torch.float32 and w.shape[1] == K and out.shape == (M, N_)
+    rc = lib().vggt_linear_f32(_p(a), _ld(a), _p(w), _ld(w), _p(bias), M, N_, K, act_in, epi, _p(out), _ld(out),
+                               _p(gamma), _stream())
+    _check(rc, "vggt_linear_f32")
+    return out
+
+
+def attention_small(q, k, v, o, batch: int, heads: int, nq: int, nk: int, D: int, q_bstride: int, k_bstride: int,
+                    o_bstride: int, scale: Optional[float] = None) -> None:
+    _dev(q, "attention_small")
+    sc = D ** -0.5 if scale is None else scale
+    rc = lib().vggt_attention_small(_p(q), _ld(q), q_bstride, _p(k), _ld(k), k_bstride, _p(v), _ld(v), _p(o), _ld(o),
+                                    o_bstride, _dt(q), batch, heads, nq, nk, D, float(sc), _stream())
+    _check(rc, "vggt_attention_small")
+
+
+def headnorm_rope_any(buf: torch.Tensor, col_off: int, H: int, D: int, w, b, eps: float, mode: int = ROPE_NONE,
+                      pos=None, period: int = 1, cos=None, sin=None) -> None:
+    """Dispatch on dtype: bf16 -> vectorised kernel (D in {64,128}); f32 -> generic kernel."""
+    if buf.dtype == torch.bfloat16:
+        return headnorm_rope(buf, col_off, H, D, w, b, eps, mode, pos, period, cos, sin)
+    _dev(buf, "headnorm_rope_f32")
+    tab = cos.shape[0] if cos is not None else 0
+    rc = lib().vggt_headnorm_rope_f32(_p(buf), _ld(buf), col_off, buf.shape[0], H, D, _p(w), _p(b), float(eps), mode,
+                                      _p(pos), period, _p(cos), _p(sin), tab, _stream())
+    _check(rc, "vggt_headnorm_rope_f32")
+
+
+def cast_f32_bf16(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    _dev(x, "cast_f32_bf16")
+    rc = lib().vggt_cast_f32_bf16(_p(x), _ld(x), _p(out), _ld(out), x.shape[0], x.shape[1], _stream())
+    _check(rc, "vggt_cast_f32_bf16")
+    return out
+
+
+def conv2d_f32(x: torch.Tensor, nimg: int, hi: int, wi: int, ci: int, w: torch.Tensor, bias, co: int, kh: int, kw: int,
+               stride: int, pad: int, y: torch.Tensor, relu_in: bool = False, relu_out: bool = False,
+               res1: Optional[torch.Tensor] = None, res1_relu: bool = False, res2: Optional[torch.Tensor] = None,
+               pos: Optional[torch.Tensor] = None, shuffle: int = 0) -> torch.Tensor:
+    """x, y, res*: 2-D [pixels, channels] row views (NHWC flattened)."""
+    _dev(x, "conv2d_f32")
+    rc = lib().vggt_conv2d_f32(_p(x), _ld(x), nimg, hi, wi, ci, _p(w), _p(bias), co, kh, kw, stride, pad, _p(y), _ld(y),
+                               int(relu_in), int(relu_out), _p(res1), _ld(res1) if res1 is not None else 0,
+                               int(res1_relu), _p(res2), _ld(res2) if res2 is not None else 0, _p(pos), shuffle,
+                               _stream())
+    _check(rc, "vggt_conv2d_f32")
+    return y
+
+
+def upsample_bilinear_f32(x: torch.Tensor, nimg: int, hi: int, wi: int, C: int, y: torch.Tensor, ho: int, wo: int,
+                          pos: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _dev(x, "upsample_bilinear_f32")
+    rc = lib().vggt_upsample_bilinear_f32(_p(x), nimg, hi, wi, C, _p(y), ho, wo, _p(pos), _stream())
+    _check(rc, "vggt_upsample_bilinear_f32")
+    return y
+
+
+def dpt_activate(x: torch.Tensor, npix: int, ppi: int, ncl: int, act: int, scale, pts: torch.Tensor,
+                 conf: torch.Tensor) -> None:
+    _dev(x, "dpt_activate")
+    rc = lib().vggt_dpt_activate(_p(x), _ld(x), npix, ppi, ncl, act, _p(scale), _p(pts), _p(conf), _stream())
+    _check(rc, "vggt_dpt_activate")

@@ -1,0 +1,259 @@
+"""VGGT DPTHead (ext ``heads/dpt_head.py`` + ``heads/utils.py``; depth head
+at featureAligned_vggt.py:166, point head at :183 / pointAligned :70) on the
+HIP fp32 tier (autocast disabled in the reference, featureAligned_vggt.py:104).
+
+All activations are NHWC fp32 rows in HBM; every convolution is one
+vggt_conv2d_f32 launch (exact-f32 MFMA implicit GEMM) with the surrounding
+elementwise work fused into it: the positional embedding add after the 1x1
+projections, the stride==kernel ConvTranspose2d as a pixel-shuffle store,
+the in-place-ReLU semantics of ResidualConvUnit (relu on the conv input,
+relu on the output, relu'd skip add) and the FeatureFusionBlock residual.
+Module names (norm, projects, resize_layers, scratch.layer*_rn,
+scratch.refinenet*, scratch.output_conv*) follow the reference checkpoint.
+All frames of a chunk are processed at once (288 GB of HBM; the reference
+chunks 8 frames at a time only to bound memory -- the arithmetic is identical).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from .. import _native as N
+from ..runtime import Workspace
+
+
+def _make_sincos(embed_dim: int, pos: torch.Tensor, omega_0: float = 100) -> torch.Tensor:
+    omega = torch.arange(embed_dim // 2, dtype=torch.double)
+    omega /= embed_dim / 2.0
+    omega = 1.0 / omega_0 ** omega
+    out = torch.einsum("m,d->md", pos.reshape(-1), omega)
+    return torch.cat([torch.sin(out), torch.cos(out)], dim=1).float()
+
+
+def _uv_grid(width: int, height: int, aspect_ratio: float) -> torch.Tensor:
+    diag = (aspect_ratio ** 2 + 1.0) ** 0.5
+    span_x, span_y = aspect_ratio / diag, 1.0 / diag
+    xs = torch.linspace(-span_x * (width - 1) / width, span_x * (width - 1) / width, steps=width)
+    ys = torch.linspace(-span_y * (height - 1) / height, span_y * (height - 1) / height, steps=height)
+    uu, vv = torch.meshgrid(xs, ys, indexing="xy")
+    return torch.stack((uu, vv), dim=-1)
+
+
+def pos_table(C: int, h: int, w: int, W_img: int, H_img: int, ratio: float = 0.1) -> torch.Tensor:
+    """DPTHead._apply_pos_embed as an NHWC table [h*w, C] (host-side constant)."""
+    grid = _uv_grid(w, h, W_img / H_img).reshape(-1, 2)
+    emb = torch.cat([_make_sincos(C // 2, grid[:, 0]), _make_sincos(C // 2, grid[:, 1])], dim=-1)
+    return (emb * ratio).contiguous()
+
+
+class ResidualConvUnit(nn.Module):
+    def __init__(self, features, activation=None, bn=False, groups=1):
+        super().__init__()
+        self.bn = bn
+        self.groups = groups
+        self.conv1 = nn.Conv2d(features, features, kernel_size=3, stride=1, padding=1, bias=True, groups=groups)
+        self.conv2 = nn.Conv2d(features, features, kernel_size=3, stride=1, padding=1, bias=True, groups=groups)
+        self.norm1 = None
+        self.norm2 = None
+        self.activation = activation
+
+
+class FeatureFusionBlock(nn.Module):
+    def __init__(self, features, activation=None, deconv=False, bn=False, expand=False, align_corners=True,
+                 size=None, has_residual=True, groups=1):
+        super().__init__()
+        self.deconv = deconv
+        self.align_corners = align_corners
+        self.groups = groups
+        self.expand = expand
+        out_features = features // 2 if expand else features
+        self.out_conv = nn.Conv2d(features, out_features, kernel_size=1, stride=1, padding=0, bias=True, groups=groups)
+        if has_residual:
+            self.resConfUnit1 = ResidualConvUnit(features, activation, bn, groups=groups)
+        self.has_residual = has_residual
+        self.resConfUnit2 = ResidualConvUnit(features, activation, bn, groups=groups)
+        self.size = size
+
+
+def _fusion(features: int, has_residual: bool = True) -> FeatureFusionBlock:
+    return FeatureFusionBlock(features, nn.ReLU(inplace=True), deconv=False, bn=False, expand=False,
+                              align_corners=True, size=None, has_residual=has_residual)
+
+
+def _scratch(in_shape, out_shape) -> nn.Module:
+    s = nn.Module()
+    s.layer1_rn = nn.Conv2d(in_shape[0], out_shape, kernel_size=3, stride=1, padding=1, bias=False)
+    s.layer2_rn = nn.Conv2d(in_shape[1], out_shape, kernel_size=3, stride=1, padding=1, bias=False)
+    s.layer3_rn = nn.Conv2d(in_shape[2], out_shape, kernel_size=3, stride=1, padding=1, bias=False)
+    s.layer4_rn = nn.Conv2d(in_shape[3], out_shape, kernel_size=3, stride=1, padding=1, bias=False)
+    return s
+
+
+def _pack_conv(conv: nn.Module, transpose: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Conv2d [co,ci,kh,kw] -> [roundup(co,64), kh*kw*ci]; ConvTranspose2d
+    [ci,co,k,k] -> [roundup(k*k*co,64), ci] with column (ky*k+kx)*co + c."""
+    w = conv.weight
+    key = (w.data_ptr(), w._version, transpose)
+    c = conv.__dict__.get("_mi355x_conv")
+    if c is not None and c[0] == key:
+        return c[1], c[2]
+    with torch.no_grad():
+        if transpose:
+            ci, co, kh, kw = w.shape
+            wp = w.detach().float().permute(2, 3, 1, 0).reshape(kh * kw * co, ci)
+        else:
+            co, ci, kh, kw = w.shape
+            wp = w.detach().float().permute(0, 2, 3, 1).reshape(co, kh * kw * ci)
+        rows = (wp.shape[0] + 63) // 64 * 64
+        if rows != wp.shape[0]:
+            wp = torch.cat([wp, wp.new_zeros(rows - wp.shape[0], wp.shape[1])], 0)
+        b = conv.bias.detach().float().contiguous() if conv.bias is not None else None
+        c = (key, wp.contiguous(), b)
+    conv.__dict__["_mi355x_conv"] = c
+    return c[1], c[2]
+
+
+class _Map:
+    """An NHWC activation: rows [n*h*w, c] fp32."""
+
+    __slots__ = ("t", "n", "h", "w", "c")
+
+    def __init__(self, t, n, h, w, c):
+        self.t, self.n, self.h, self.w, self.c = t, n, h, w, c
+
+
+def _conv(x: _Map, conv: nn.Conv2d, stride=1, pad=None, relu_in=False, relu_out=False, res1: _Map = None,
+          res1_relu=False, res2: _Map = None, pos=None) -> _Map:
+    wp, b = _pack_conv(conv)
+    co, _, kh, kw = conv.weight.shape
+    pad = conv.padding[0] if pad is None else pad
+    ho = (x.h + 2 * pad - kh) // stride + 1
+    wo = (x.w + 2 * pad - kw) // stride + 1
+    y = torch.empty(x.n * ho * wo, co, device=x.t.device)
+    N.conv2d_f32(x.t, x.n, x.h, x.w, x.c, wp, b, co, kh, kw, stride, pad, y, relu_in, relu_out,
+                 res1.t if res1 else None, res1_relu, res2.t if res2 else None, pos)
+    return _Map(y, x.n, ho, wo, co)
+
+
+def _convT(x: _Map, conv: nn.ConvTranspose2d) -> _Map:
+    wp, b = _pack_conv(conv, transpose=True)
+    ci, co, k, _ = conv.weight.shape
+    assert conv.stride[0] == k and conv.padding[0] == 0
+    y = torch.empty(x.n * x.h * k * x.w * k, co, device=x.t.device)
+    N.conv2d_f32(x.t, x.n, x.h, x.w, x.c, wp, b, co, 1, 1, 1, 0, y, shuffle=k)
+    return _Map(y, x.n, x.h * k, x.w * k, co)
+
+
+def _upsample(x: _Map, ho: int, wo: int, pos=None) -> _Map:
+    y = torch.empty(x.n * ho * wo, x.c, device=x.t.device)
+    N.upsample_bilinear_f32(x.t, x.n, x.h, x.w, x.c, y, ho, wo, pos)
+    return _Map(y, x.n, ho, wo, x.c)
+
+
+class DPTHead(nn.Module):
+    def __init__(self, dim_in: int, patch_size: int = 14, output_dim: int = 4, activation: str = "inv_log",
+                 conf_activation: str = "expp1", features: int = 256, out_channels=(256, 512, 1024, 1024),
+                 intermediate_layer_idx=(4, 11, 17, 23), pos_embed: bool = True, feature_only: bool = False,
+                 down_ratio: int = 1):
+        super().__init__()
+        if feature_only or down_ratio != 1:
+            raise NotImplementedError("feature_only / down_ratio are not used by any reference model")
+        if activation not in ("exp", "inv_log") or conf_activation != "expp1":
+            raise NotImplementedError(f"activation {activation}/{conf_activation}")
+        self.patch_size = patch_size
+        self.activation = activation
+        self.conf_activation = conf_activation
+        self.pos_embed = pos_embed
+        self.feature_only = feature_only
+        self.down_ratio = down_ratio
+        self.intermediate_layer_idx = list(intermediate_layer_idx)
+        self.output_dim = output_dim
+        out_channels = list(out_channels)
+        self.out_channels = out_channels
+        self.norm = nn.LayerNorm(dim_in)
+        self.projects = nn.ModuleList([nn.Conv2d(dim_in, oc, kernel_size=1, stride=1, padding=0) for oc in out_channels])
+        self.resize_layers = nn.ModuleList([
+            nn.ConvTranspose2d(out_channels[0], out_channels[0], kernel_size=4, stride=4, padding=0),
+            nn.ConvTranspose2d(out_channels[1], out_channels[1], kernel_size=2, stride=2, padding=0),
+            nn.Identity(),
+            nn.Conv2d(out_channels[3], out_channels[3], kernel_size=3, stride=2, padding=1)])
+        self.scratch = _scratch(out_channels, features)
+        self.scratch.stem_transpose = None
+        self.scratch.refinenet1 = _fusion(features)
+        self.scratch.refinenet2 = _fusion(features)
+        self.scratch.refinenet3 = _fusion(features)
+        self.scratch.refinenet4 = _fusion(features, has_residual=False)
+        self.scratch.output_conv1 = nn.Conv2d(features, features // 2, kernel_size=3, stride=1, padding=1)
+        self.scratch.output_conv2 = nn.Sequential(
+            nn.Conv2d(features // 2, 32, kernel_size=3, stride=1, padding=1), nn.ReLU(inplace=True),
+            nn.Conv2d(32, output_dim, kernel_size=1, stride=1, padding=0))
+
+    def _pos(self, C: int, h: int, w: int, W_img: int, H_img: int, device) -> torch.Tensor:
+        cache = self.__dict__.setdefault("_mi355x_pos", {})
+        key = (C, h, w, W_img, H_img, str(device))
+        if key not in cache:
+            cache[key] = pos_table(C, h, w, W_img, H_img).to(device)
+        return cache[key]
+
+    def _fuse(self, blk: FeatureFusionBlock, x0: _Map, x1: Optional[_Map], size) -> _Map:
+        out = x0
+        if x1 is not None:
+            t = _conv(x1, blk.resConfUnit1.conv1, relu_in=True, relu_out=True)
+            out = _conv(t, blk.resConfUnit1.conv2, res1=x1, res1_relu=True, res2=x0)
+        t = _conv(out, blk.resConfUnit2.conv1, relu_in=True, relu_out=True)
+        out = _conv(t, blk.resConfUnit2.conv2, res1=out, res1_relu=True)
+        ho, wo = size if size is not None else (out.h * 2, out.w * 2)
+        return _conv(_upsample(out, ho, wo), blk.out_conv)
+
+    @torch.no_grad()
+    def forward(self, aggregated_tokens_list: List[torch.Tensor], images: torch.Tensor, patch_start_idx: int,
+                frames_chunk_size: int = 8, _scale: Optional[torch.Tensor] = None):
+        """-> (preds (B,S,H,W,output_dim-1), conf (B,S,H,W)).  ``_scale`` (B,)
+        optionally multiplies preds (the chunk-scale fusion of
+        featureAligned_vggt.py:171)."""
+        B, S, _, H, W = images.shape
+        if images.device.type != "cuda":
+            raise RuntimeError("DPTHead: the MI355X hot path runs on HIP devices only (no CPU fallback)")
+        dev = images.device
+        ph, pw = H // self.patch_size, W // self.patch_size
+        F_ = B * S
+        hw = ph * pw
+        ws = Workspace.get(dev)
+        feats = []
+        for li, layer_idx in enumerate(self.intermediate_layer_idx):
+            tk = aggregated_tokens_list[layer_idx]
+            P, Cin = tk.shape[2], tk.shape[3]
+            xl = ws.buf("dpt_ln", F_ * hw, Cin)
+            N.layernorm_grouped(tk.reshape(F_ * P, Cin), self.norm.weight, self.norm.bias, self.norm.eps, xl, F_ * hw,
+                                Cin, hw, P, patch_start_idx, hw, 0)
+            oc = self.out_channels[li]
+            pos = self._pos(oc, ph, pw, W, H, dev) if self.pos_embed else None
+            x = _conv(_Map(xl, F_, ph, pw, Cin), self.projects[li], pos=pos)
+            if li == 0 or li == 1:
+                x = _convT(x, self.resize_layers[li])
+            elif li == 3:
+                x = _conv(x, self.resize_layers[3], stride=2, pad=1)
+            feats.append(x)
+        sc = self.scratch
+        l1 = _conv(feats[0], sc.layer1_rn)
+        l2 = _conv(feats[1], sc.layer2_rn)
+        l3 = _conv(feats[2], sc.layer3_rn)
+        l4 = _conv(feats[3], sc.layer4_rn)
+        out = self._fuse(sc.refinenet4, l4, None, (l3.h, l3.w))
+        out = self._fuse(sc.refinenet3, out, l3, (l2.h, l2.w))
+        out = self._fuse(sc.refinenet2, out, l2, (l1.h, l1.w))
+        out = self._fuse(sc.refinenet1, out, l1, None)
+        out = _conv(out, sc.output_conv1)
+        Ho, Wo = int(ph * self.patch_size / self.down_ratio), int(pw * self.patch_size / self.down_ratio)
+        out = _upsample(out, Ho, Wo, self._pos(out.c, Ho, Wo, W, H, dev) if self.pos_embed else None)
+        out = _conv(out, sc.output_conv2[0], relu_out=True)
+        out = _conv(out, sc.output_conv2[2])
+        ncl = self.output_dim
+        npix = F_ * Ho * Wo
+        preds = torch.empty(B, S, Ho, Wo, ncl - 1, device=dev)
+        conf = torch.empty(B, S, Ho, Wo, device=dev)
+        scale = _scale.float().reshape(B, 1).expand(B, S).contiguous().view(-1) if _scale is not None else None
+        N.dpt_activate(out.t, npix, Ho * Wo, ncl, 0 if self.activation == "exp" else 1, scale, preds, conf)
+        return preds, conf

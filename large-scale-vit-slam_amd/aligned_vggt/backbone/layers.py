@@ -149,3 +149,32 @@ class Block(nn.Module):
         N.gemm_bf16(xn, w, b, hid, N.EPI_GELU_BF16)
         w, b = pack_linear(self.mlp.fc2)
         N.gemm_bf16(hid, w, b, xs, N.EPI_RESID_F32, gamma=self._gamma(self.ls2, C, x.device), out2=out2)
+
+    @torch.no_grad()
+    def forward_f32(self, x: torch.Tensor) -> torch.Tensor:
+        """fp32 tier (autocast disabled, e.g. the camera-head trunk,
+        featureAligned_vggt.py:104-106): x (B, N, C) -> new x; plain
+        self-attention over the N tokens of each batch row (no QK-norm/RoPE
+        unless configured)."""
+        B, Nn, C = x.shape
+        H = self.attn.num_heads
+        D = C // H
+        dev = x.device
+        xs = x.reshape(B * Nn, C).float().contiguous().clone()
+        xn = torch.empty_like(xs)
+        N.layernorm(xs, self.norm1.weight, self.norm1.bias, self.norm1.eps, xn)
+        qkv = torch.empty(B * Nn, 3 * C, device=dev)
+        N.linear_f32(xn, self.attn.qkv.weight, self.attn.qkv.bias, qkv)
+        for off, nm in ((0, self.attn.q_norm), (C, self.attn.k_norm)):
+            if isinstance(nm, nn.LayerNorm):
+                N.headnorm_rope_any(qkv, off, H, D, nm.weight, nm.bias, nm.eps)
+        ao = torch.empty(B * Nn, C, device=dev)
+        N.attention_small(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], ao, B, H, Nn, Nn, D, Nn, Nn, Nn)
+        N.linear_f32(ao, self.attn.proj.weight, self.attn.proj.bias, xs, N.EPI_RESID_F32,
+                     gamma=self._gamma(self.ls1, C, dev))
+        N.layernorm(xs, self.norm2.weight, self.norm2.bias, self.norm2.eps, xn)
+        hid = torch.empty(B * Nn, self.mlp.fc1.out_features, device=dev)
+        N.linear_f32(xn, self.mlp.fc1.weight, self.mlp.fc1.bias, hid, N.EPI_GELU_BF16)
+        N.linear_f32(hid, self.mlp.fc2.weight, self.mlp.fc2.bias, xs, N.EPI_RESID_F32,
+                     gamma=self._gamma(self.ls2, C, dev))
+        return xs.view(B, Nn, C)

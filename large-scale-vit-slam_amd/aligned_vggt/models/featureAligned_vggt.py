@@ -1,0 +1,182 @@
+"""FeatureAlignedVGGT (aligned_vggt/models/featureAligned_vggt.py:16-254) on
+MI355X: same constructor, ``set_config``, ``forward(images, num_overlap,
+context=None, gt_poses=None) -> dict`` with the reference's in-place
+``context`` semantics, and the same state-dict names, so
+training/run_model.py can instantiate and call it unchanged.
+
+Per chunk: HIP aggregator (only layers 4/11/17/23 materialised) -> HIP
+alignment head -> HIP camera head / DPT depth (+ point) heads; the Sim(3)/SE(3)
+composition of featureAligned_vggt.py:96-143 is small per-frame device glue.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..backbone.aggregator import Aggregator
+from ..backbone.camera_head import CameraHead
+from ..backbone.dpt_head import DPTHead
+from ..backbone.track_head import TrackHead
+from ..heads.alignment_head import AlignmentHead
+from ..utils.data import extri_to_pose_encoding, pose_encoding_to_extri
+from ..utils.geometry import averagePoseEncodings, closed_form_inverse_se3
+from ..utils.pose_enc import extri_intri_to_pose_encoding, pose_encoding_to_extri_intri
+
+try:  # optional, as in the reference (featureAligned_vggt.py:3); only used for from_pretrained
+    from huggingface_hub import PyTorchModelHubMixin
+except Exception:  # pragma: no cover
+    class PyTorchModelHubMixin:  # type: ignore
+        pass
+
+
+class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
+    def __init__(self, img_size=518, patch_size=14, embed_dim=1024, enable_camera=True, enable_point=True,
+                 enable_depth=True, enable_track=True, num_memory_tokens=8, temporal_attention=True):
+        super().__init__()
+        self.embed_dim = embed_dim
+        self.enable_memory = num_memory_tokens > 0
+        self.intermediate_layer_indices = [4, 11, 17, 23]
+        self.aggregator = Aggregator(img_size=img_size, patch_size=patch_size, embed_dim=embed_dim)
+        n = len(self.intermediate_layer_indices)
+        self.camera_head = CameraHead(dim_in=2 * embed_dim) if enable_camera else None
+        self.point_head = DPTHead(dim_in=2 * embed_dim, output_dim=4, activation="inv_log", conf_activation="expp1",
+                                  intermediate_layer_idx=range(n)) if enable_point else None
+        self.depth_head = DPTHead(dim_in=2 * embed_dim, output_dim=2, activation="exp", conf_activation="expp1",
+                                  intermediate_layer_idx=range(n)) if enable_depth else None
+        self.track_head = TrackHead(dim_in=2 * embed_dim, patch_size=patch_size) if enable_track else None
+        self.alignment_head = AlignmentHead(in_dim=2 * embed_dim, patch_size=patch_size,
+                                            num_memory_tokens=num_memory_tokens,
+                                            temporal_attention=temporal_attention)
+
+    def set_config(self, cfg):
+        """featureAligned_vggt.py:34-46 (re-creates the alignment head with
+        fresh weights, as the reference does; load weights afterwards)."""
+        self.camera_head = self.camera_head if cfg.enable_camera else None
+        self.point_head = self.point_head if cfg.enable_point else None
+        self.depth_head = self.depth_head if cfg.enable_depth else None
+        self.track_head = self.track_head if cfg.enable_track else None
+        self.enable_memory = cfg.num_memory_tokens > 0
+        dev = next(self.aggregator.parameters()).device
+        self.alignment_head = AlignmentHead(in_dim=2 * self.embed_dim, patch_size=cfg.patch_size,
+                                            num_memory_tokens=cfg.num_memory_tokens,
+                                            temporal_attention=cfg.temporal_attention).to(dev)
+
+    @torch.no_grad()
+    def forward(self, images: torch.Tensor, num_overlap: int, context: dict = None, gt_poses: torch.Tensor = None) -> dict:
+        B, S, C, H, W = images.shape
+        predictions = {}
+        toks, patch_start_idx = self.aggregator(images, keep_layers=self.intermediate_layer_indices)
+
+        ctx_overlap = ctx_memory = None
+        if context is not None:
+            ctx_overlap = context["overlap_tokens"]
+            if self.enable_memory:
+                ctx_memory = context["memory_tokens"][-1]
+        overlap = num_overlap if S > num_overlap else S - 1
+        chunk_sim3_enc, frame_se3_enc, memory_tokens, overlap_tokens = self.alignment_head(
+            toks[-1], (H, W), overlap, overlap_tokens=ctx_overlap, memory_tokens=ctx_memory)
+
+        chunk_se3 = pose_encoding_to_extri(chunk_sim3_enc)
+        chunk_scale = chunk_sim3_enc[..., -1]
+        per_frame_se3 = torch.matmul(pose_encoding_to_extri(frame_se3_enc), chunk_se3)
+        per_frame_se3 = torch.cat([chunk_se3, per_frame_se3], dim=1)
+
+        point_identity_alignment = None
+        if self.camera_head is not None:
+            pose_enc_list = self.camera_head(toks)
+            extr, intr = pose_encoding_to_extri_intri(pose_enc_list[-1], image_size_hw=images.shape[-2:])
+            extr = F.pad(extr, (0, 0, 0, 1, 0, 0, 0, 0), mode="constant")
+            extr[:, :, 3, 3] = 1.0
+            ident = closed_form_inverse_se3(extr[:, 0])
+            point_identity_alignment = extr[:, 0].detach().clone()
+            extr = extr @ ident.view(B, 1, 4, 4)
+            extr[:, :, :3, 3] *= chunk_scale.view(B, 1, 1)
+            if context is not None:
+                if gt_poses is not None:
+                    mean_camera_transform = gt_poses[:, :1].to(extr)
+                else:
+                    ctx_o = pose_encoding_to_extri(context["pose_enc"][-1][:, -overlap:].to(extr.device))
+                    inv_o = closed_form_inverse_se3(extr[:, :overlap].reshape(B * overlap, 4, 4)).reshape(
+                        B, overlap, 4, 4)
+                    ct = inv_o @ ctx_o
+                    if overlap > 1:
+                        mean_camera_transform = pose_encoding_to_extri(averagePoseEncodings(extri_to_pose_encoding(ct)))
+                    else:
+                        mean_camera_transform = ct
+            else:
+                mean_camera_transform = torch.eye(4, device=images.device, dtype=images.dtype).view(1, 1, 4, 4).expand(
+                    B, -1, -1, -1)
+            per_frame_se3 = torch.matmul(per_frame_se3, mean_camera_transform)
+            aligned_extr = torch.matmul(extr, per_frame_se3)
+            aligned_pose_enc = extri_intri_to_pose_encoding(aligned_extr, intr, image_size_hw=images.shape[-2:])
+
+            predictions["overlap_tokens"] = overlap_tokens
+            if context is None:
+                predictions["pose_enc"] = [aligned_pose_enc]
+                predictions["chunk_sim3_alignment_enc"] = chunk_sim3_enc
+                predictions["frame_se3_alignment_enc"] = frame_se3_enc
+                if self.enable_memory:
+                    predictions["memory_tokens"] = [memory_tokens]
+            else:
+                context.setdefault("pose_enc", []).append(aligned_pose_enc)
+                predictions["pose_enc"] = context["pose_enc"]
+                predictions["chunk_sim3_alignment_enc"] = merge_results(context["chunk_sim3_alignment_enc"],
+                                                                        chunk_sim3_enc, 0, 1)
+                predictions["frame_se3_alignment_enc"] = merge_results(context["frame_se3_alignment_enc"],
+                                                                       frame_se3_enc, 0, 1)
+                if self.enable_memory:
+                    context.setdefault("memory_tokens", []).append(memory_tokens)
+                    predictions["memory_tokens"] = context["memory_tokens"]
+
+        if self.depth_head is not None:
+            depth, depth_conf = self.depth_head(toks, images=images, patch_start_idx=patch_start_idx,
+                                                _scale=chunk_scale.reshape(B))
+            if context is None:
+                predictions["depth"] = [depth]
+                predictions["depth_conf"] = [depth_conf]
+            else:
+                context.setdefault("depth", []).append(depth)
+                predictions["depth"] = context["depth"]
+                context.setdefault("depth_conf", []).append(depth_conf)
+                predictions["depth_conf"] = context["depth_conf"]
+
+        if self.point_head is not None:
+            pts3d, pts3d_conf = self.point_head(toks, images=images, patch_start_idx=patch_start_idx)
+            if self.camera_head is not None:
+                if context is not None:
+                    pt = closed_form_inverse_se3(per_frame_se3[:, 0]).unsqueeze(1)
+                    pt = pt @ point_identity_alignment.view(B, 1, 4, 4)
+                else:
+                    pt = point_identity_alignment.view(B, 1, 4, 4)
+                pts3d = pts3d * chunk_scale.view(B, 1, 1, 1, 1)
+                R = pt[:, 0, :3, :3]
+                t = pt[:, 0, :3, 3]
+                pts3d = (pts3d.reshape(B, -1, 3) @ R.transpose(-1, -2) + t[:, None]).view(B, S, H, W, 3)
+            if context is None:
+                predictions["world_points"] = [pts3d]
+                predictions["world_points_conf"] = [pts3d_conf]
+            else:
+                context.setdefault("world_points", []).append(pts3d)
+                predictions["world_points"] = context["world_points"]
+                context.setdefault("world_points_conf", []).append(pts3d_conf)
+                predictions["world_points_conf"] = context["world_points_conf"]
+
+        if not self.training:
+            if context is None:
+                predictions["images"] = [images]
+            else:
+                context.setdefault("images", []).append(images)
+                predictions["images"] = context["images"]
+        return predictions
+
+
+def merge_results(first_chunk, second_chunk, num_overlap: int = 0, mergeDim: int = 1):
+    """featureAligned_vggt.py:227-254."""
+    if isinstance(first_chunk, list) and isinstance(second_chunk, list):
+        if num_overlap > 0:
+            second_chunk = [item[:, num_overlap:] for item in second_chunk]
+        return [torch.cat((a, b), dim=mergeDim) for a, b in zip(first_chunk, second_chunk)]
+    if num_overlap > 0:
+        second_chunk = second_chunk[:, num_overlap:]
+    return torch.cat((first_chunk, second_chunk), dim=mergeDim)

@@ -1,0 +1,284 @@
+// DPT head convolutions (include/vggt_mi355x.h: vggt_conv2d_f32,
+// vggt_upsample_bilinear_f32, vggt_dpt_activate).
+//
+// The reference runs the DPT heads with autocast disabled
+// (featureAligned_vggt.py:104), i.e. in fp32; so does this path: an implicit
+// GEMM over NHWC activations with exact-f32 MFMA (v_mfma_f32_16x16x4_f32).
+//   out[pixel, co] = sum_{ky,kx,ci} act(x[pixel@(ky,kx), ci]) * W[co, ky, kx, ci]
+// K is ordered (ky, kx, ci) with Ci % 32 == 0, so every 32-wide K slice is one
+// tap and a contiguous channel run (16-B loads, zero for padding taps).
+// Block tile 128 pixels x 64 channels x 32 K, 4 waves (2x2), register-staged
+// double buffer through XOR-swizzled LDS.  Fused epilogue: bias, ReLU,
+// up to two residual adds (one optionally ReLU'd: the in-place-ReLU skip of
+// DPT's ResidualConvUnit), a per-pixel positional table, and the
+// pixel-shuffle store of a stride == kernel ConvTranspose2d.
+#include <math.h>
+
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 64, BK = 32, NT = 256;
+
+struct ConvArgs {
+  const float* x;
+  const float* w;
+  const float* bias;
+  float* y;
+  const float* res1;
+  const float* res2;
+  const float* pos;
+  int64_t ldx, ldy, ldr1, ldr2;
+  int nimg, hi, wi, ci, ho, wo, co, kh, kw, stride, pad;
+  int relu_in, relu_out, res1_relu;
+  int shuffle;  // >0: ConvT pixel shuffle factor s; co is then the per-tap output channels
+  int ncols;    // GEMM N (= co, or s*s*co for the shuffle)
+};
+
+__global__ __launch_bounds__(NT, 2) void conv_f32_kernel(ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) float As[2][BM * BK];
+  __shared__ __attribute__((aligned(16))) float Ws[2][BN * BK];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int M = a.nimg * a.ho * a.wo;
+  const int tiles_n = (a.ncols + BN - 1) / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (t / tiles_n) * BM;
+  const int n0 = (t % tiles_n) * BN;
+  const int K = a.kh * a.kw * a.ci;
+  const int nk = K / BK;
+
+  // per-thread A rows: r = tid/8 + 32*i, channel quad c4 = tid%8
+  const int c4 = tid & 7;
+  int pn[4], py[4], px[4];
+  bool pv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + (tid >> 3) + 32 * i;
+    pv[i] = m < M;
+    const int mm = pv[i] ? m : 0;
+    pn[i] = mm / (a.ho * a.wo);
+    const int rem = mm % (a.ho * a.wo);
+    py[i] = (rem / a.wo) * a.stride - a.pad;
+    px[i] = (rem % a.wo) * a.stride - a.pad;
+  }
+  // per-thread W rows: r = tid/8 + 32*i (i < 2)
+  f32x4 ra[4], rw[2];
+
+  auto load = [&](int kt) {
+    const int k0 = kt * BK;
+    const int tap = k0 / a.ci;
+    const int ci0 = k0 % a.ci + c4 * 4;
+    const int ky = tap / a.kw, kx = tap % a.kw;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int iy = py[i] + ky, ix = px[i] + kx;
+      if (pv[i] && iy >= 0 && iy < a.hi && ix >= 0 && ix < a.wi) {
+        f32x4 v = *(const f32x4*)(a.x + (((int64_t)pn[i] * a.hi + iy) * a.wi + ix) * a.ldx + ci0);
+        if (a.relu_in) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+        }
+        ra[i] = v;
+      } else {
+        ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int n = n0 + (tid >> 3) + 32 * i;  // weights are padded to a multiple of BN rows
+      rw[i] = *(const f32x4*)(a.w + (int64_t)n * K + k0 + c4 * 4);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      *(f32x4*)(&As[buf][r * BK + ((c4 ^ (r & 7)) << 2)]) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      *(f32x4*)(&Ws[buf][r * BK + ((c4 ^ (r & 7)) << 2)]) = rw[i];
+    }
+  };
+
+  const int wm = wave >> 1, wn = wave & 1;
+  const int r16 = lane & 15, q = lane >> 4;
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load(kt + 1);
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      const int ch = kc * 4 + q;
+      f32x4 af[4], wf[2];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int r = wm * 64 + mt * 16 + r16;
+        af[mt] = *(const f32x4*)(&As[cur][r * BK + ((ch ^ (r & 7)) << 2)]);
+      }
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int r = wn * 32 + nt * 16 + r16;
+        wf[nt] = *(const f32x4*)(&Ws[cur][r * BK + ((ch ^ (r & 7)) << 2)]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mt][j], wf[nt][j], acc[mt][nt], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds C[m = 4q + i][n = r16] of each 16x16 tile ----
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int n = n0 + wn * 32 + nt * 16 + r16;
+    if (n >= a.ncols) continue;
+    int co = n, dy = 0, dx = 0;
+    if (a.shuffle) {
+      const int tap = n / a.co;
+      co = n % a.co;
+      dy = tap / a.shuffle;
+      dx = tap % a.shuffle;
+    }
+    const float bv = a.bias ? a.bias[co] : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm * 64 + mt * 16 + 4 * q + i;
+        if (m >= M) continue;
+        float v = acc[mt][nt][i] + bv;
+        if (a.relu_out) v = fmaxf(v, 0.f);
+        int64_t opix;
+        if (a.shuffle) {
+          const int img = m / (a.ho * a.wo), rem = m % (a.ho * a.wo);
+          const int oy = (rem / a.wo) * a.shuffle + dy, ox = (rem % a.wo) * a.shuffle + dx;
+          opix = ((int64_t)img * a.ho * a.shuffle + oy) * (a.wo * a.shuffle) + ox;
+        } else {
+          opix = m;
+          if (a.pos) v += a.pos[(int64_t)(m % (a.ho * a.wo)) * a.co + co];
+          if (a.res1) {
+            const float r = a.res1[(int64_t)m * a.ldr1 + co];
+            v += a.res1_relu ? fmaxf(r, 0.f) : r;
+          }
+          if (a.res2) v += a.res2[(int64_t)m * a.ldr2 + co];
+        }
+        a.y[opix * a.ldy + co] = v;
+      }
+  }
+}
+
+// Bilinear resize, align_corners=True, NHWC f32 (F.interpolate semantics),
+// optional positional table [ho*wo, C] added to the result.
+__global__ __launch_bounds__(256) void upsample_kernel(const float* __restrict__ x, int nimg, int hi, int wi, int C,
+                                                       float* __restrict__ y, int ho, int wo,
+                                                       const float* __restrict__ pos) {
+  const int c4n = C / 4;
+  const int64_t total = (int64_t)nimg * ho * wo * c4n;
+  const float sh = ho > 1 ? (float)(hi - 1) / (float)(ho - 1) : 0.f;
+  const float sw = wo > 1 ? (float)(wi - 1) / (float)(wo - 1) : 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % c4n) * 4;
+    const int64_t p = i / c4n;
+    const int img = (int)(p / ((int64_t)ho * wo));
+    const int rem = (int)(p % ((int64_t)ho * wo));
+    const int oy = rem / wo, ox = rem % wo;
+    const float fy = sh * oy, fx = sw * ox;
+    const int y0 = (int)fy, x0 = (int)fx;
+    const int y1 = min(y0 + 1, hi - 1), x1 = min(x0 + 1, wi - 1);
+    const float ly = fy - y0, lx = fx - x0;
+    const float hy = 1.f - ly, hx = 1.f - lx;
+    const float* b = x + (int64_t)img * hi * wi * C;
+    const f32x4 v00 = *(const f32x4*)(b + ((int64_t)y0 * wi + x0) * C + c);
+    const f32x4 v01 = *(const f32x4*)(b + ((int64_t)y0 * wi + x1) * C + c);
+    const f32x4 v10 = *(const f32x4*)(b + ((int64_t)y1 * wi + x0) * C + c);
+    const f32x4 v11 = *(const f32x4*)(b + ((int64_t)y1 * wi + x1) * C + c);
+    f32x4 o = hy * (hx * v00 + lx * v01) + ly * (hx * v10 + lx * v11);
+    if (pos) o += *(const f32x4*)(pos + (int64_t)rem * C + c);
+    *(f32x4*)(y + p * C + c) = o;
+  }
+}
+
+// DPT activate_head: x [P, ncl] NHWC (last channel = confidence).
+//   act 0: exp, 1: inv_log (sign(x)*expm1(|x|)); conf: 1 + exp(c) (expp1).
+//   pts[p, j] = act(x[p, j]) * scale[img]   (j < ncl-1),  conf[p] = 1 + exp(x[p, ncl-1])
+__global__ __launch_bounds__(256) void dpt_act_kernel(const float* __restrict__ x, int64_t ldx, int64_t npix,
+                                                      int ppi, int ncl, int act, const float* __restrict__ scale,
+                                                      float* __restrict__ pts, float* __restrict__ conf) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
+    const float s = scale ? scale[p / ppi] : 1.f;
+    for (int j = 0; j < ncl - 1; ++j) {
+      const float v = x[p * ldx + j];
+      const float a = act == 0 ? expf(v) : copysignf(expm1f(fabsf(v)), v) * (v == 0.f ? 0.f : 1.f);
+      pts[p * (ncl - 1) + j] = a * s;
+    }
+    conf[p] = 1.f + expf(x[p * ldx + ncl - 1]);
+  }
+}
+
+inline int grid_for(int64_t total) {
+  int64_t g = (total + 255) / 256;
+  return (int)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
+}
+
+}  // namespace
+
+extern "C" int vggt_conv2d_f32(const float* x, int64_t ldx, int nimg, int hi, int wi, int ci, const float* w,
+                               const float* bias, int co, int kh, int kw, int stride, int pad, float* y, int64_t ldy,
+                               int relu_in, int relu_out, const float* res1, int64_t ldr1, int res1_relu,
+                               const float* res2, int64_t ldr2, const float* pos, int shuffle, void* stream) {
+  if (nimg <= 0 || hi <= 0 || wi <= 0 || ci <= 0 || co <= 0 || kh <= 0 || kw <= 0 || stride <= 0 || pad < 0)
+    return VGGT_ERR_SHAPE;
+  if (ci % BK) return VGGT_ERR_SHAPE;
+  if (shuffle && (kh != 1 || kw != 1 || stride != 1 || pad != 0 || res1 || res2 || pos)) return VGGT_ERR_UNSUPPORTED;
+  if ((ldx % 4) || ((uintptr_t)x % 16) || ((uintptr_t)w % 16)) return VGGT_ERR_ALIGN;
+  ConvArgs a;
+  a.x = x; a.w = w; a.bias = bias; a.y = y; a.res1 = res1; a.res2 = res2; a.pos = pos;
+  a.ldx = ldx; a.ldy = ldy; a.ldr1 = ldr1; a.ldr2 = ldr2;
+  a.nimg = nimg; a.hi = hi; a.wi = wi; a.ci = ci;
+  a.ho = (hi + 2 * pad - kh) / stride + 1;
+  a.wo = (wi + 2 * pad - kw) / stride + 1;
+  a.co = co; a.kh = kh; a.kw = kw; a.stride = stride; a.pad = pad;
+  a.relu_in = relu_in; a.relu_out = relu_out; a.res1_relu = res1_relu;
+  a.shuffle = shuffle;
+  a.ncols = shuffle ? shuffle * shuffle * co : co;
+  const int64_t M = (int64_t)nimg * a.ho * a.wo;
+  const int64_t nwg = ((M + BM - 1) / BM) * ((a.ncols + BN - 1) / BN);
+  if (nwg > 0x7fffffff) return VGGT_ERR_SHAPE;
+  conv_f32_kernel<<<(int)nwg, NT, 0, (hipStream_t)stream>>>(a);
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+extern "C" int vggt_upsample_bilinear_f32(const float* x, int nimg, int hi, int wi, int C, float* y, int ho, int wo,
+                                          const float* pos, void* stream) {
+  if (nimg <= 0 || hi <= 0 || wi <= 0 || ho <= 0 || wo <= 0 || C % 4) return VGGT_ERR_SHAPE;
+  if (((uintptr_t)x | (uintptr_t)y) % 16) return VGGT_ERR_ALIGN;
+  upsample_kernel<<<grid_for((int64_t)nimg * ho * wo * (C / 4)), 256, 0, (hipStream_t)stream>>>(x, nimg, hi, wi, C, y,
+                                                                                                 ho, wo, pos);
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+extern "C" int vggt_dpt_activate(const float* x, int64_t ldx, int64_t npix, int pix_per_img, int ncl, int act,
+                                 const float* scale, float* pts, float* conf, void* stream) {
+  if (npix <= 0 || ncl < 2 || pix_per_img <= 0 || (act != 0 && act != 1)) return VGGT_ERR_SHAPE;
+  dpt_act_kernel<<<grid_for(npix), 256, 0, (hipStream_t)stream>>>(x, ldx, npix, pix_per_img, ncl, act, scale, pts,
+                                                                  conf);
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}

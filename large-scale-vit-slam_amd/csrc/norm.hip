@@ -7,26 +7,36 @@ namespace {
 
 // ---------------------------------------------------------------- LayerNorm
 // NV = C / 256 float4 per lane (C = 256 * NV).
+// Row r of the logical [M, C] input maps to group g = r / G, i = r % G:
+//   x row = g*xgs + xoff + i,  y row = g*ygs + yoff + i   (identity: G = M).
+struct RowMap {
+  int G, xgs, xoff, ygs, yoff;
+};
+
 template <int NV, bool IN_BF16, bool OUT_BF16>
 __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__ x, int64_t ldx,
                                                         const float* __restrict__ w, const float* __restrict__ b,
-                                                        float eps, int M, void* __restrict__ y, int64_t ldy) {
+                                                        float eps, int M, void* __restrict__ y, int64_t ldy,
+                                                        RowMap rm) {
   constexpr int C = NV * 256;
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
+  const int lrow = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (lrow >= M) return;
+  const int gi = lrow / rm.G, ii = lrow % rm.G;
+  const int64_t row = (int64_t)gi * rm.xgs + rm.xoff + ii;
+  const int64_t orow = (int64_t)gi * rm.ygs + rm.yoff + ii;
   float v[NV][4];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = i * 256 + lane * 4;
     if constexpr (IN_BF16) {
-      const uint2 u = *(const uint2*)((const bf16_t*)x + (int64_t)row * ldx + c);
+      const uint2 u = *(const uint2*)((const bf16_t*)x + row * ldx + c);
       v[i][0] = bf2f(u.x & 0xffff);
       v[i][1] = bf2f(u.x >> 16);
       v[i][2] = bf2f(u.y & 0xffff);
       v[i][3] = bf2f(u.y >> 16);
     } else {
-      const f32x4 u = *(const f32x4*)((const float*)x + (int64_t)row * ldx + c);
+      const f32x4 u = *(const f32x4*)((const float*)x + row * ldx + c);
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[i][j] = u[j];
     }
@@ -63,21 +73,21 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
       uint2 u;
       u.x = pack_bf2(o[0], o[1]);
       u.y = pack_bf2(o[2], o[3]);
-      *(uint2*)((bf16_t*)y + (int64_t)row * ldy + c) = u;
+      *(uint2*)((bf16_t*)y + orow * ldy + c) = u;
     } else {
-      *(f32x4*)((float*)y + (int64_t)row * ldy + c) = f32x4{o[0], o[1], o[2], o[3]};
+      *(f32x4*)((float*)y + orow * ldy + c) = f32x4{o[0], o[1], o[2], o[3]};
     }
   }
 }
 
 template <int NV>
 int launch_ln(const void* x, int in_bf, int64_t ldx, const float* w, const float* b, float eps, int M, void* y,
-              int out_bf, int64_t ldy, hipStream_t s) {
+              int out_bf, int64_t ldy, RowMap rm, hipStream_t s) {
   const int grid = (M + 3) / 4;
-  if (in_bf && out_bf) layernorm_kernel<NV, true, true><<<grid, 256, 0, s>>>(x, ldx, w, b, eps, M, y, ldy);
-  else if (in_bf) layernorm_kernel<NV, true, false><<<grid, 256, 0, s>>>(x, ldx, w, b, eps, M, y, ldy);
-  else if (out_bf) layernorm_kernel<NV, false, true><<<grid, 256, 0, s>>>(x, ldx, w, b, eps, M, y, ldy);
-  else layernorm_kernel<NV, false, false><<<grid, 256, 0, s>>>(x, ldx, w, b, eps, M, y, ldy);
+  if (in_bf && out_bf) layernorm_kernel<NV, true, true><<<grid, 256, 0, s>>>(x, ldx, w, b, eps, M, y, ldy, rm);
+  else if (in_bf) layernorm_kernel<NV, true, false><<<grid, 256, 0, s>>>(x, ldx, w, b, eps, M, y, ldy, rm);
+  else if (out_bf) layernorm_kernel<NV, false, true><<<grid, 256, 0, s>>>(x, ldx, w, b, eps, M, y, ldy, rm);
+  else layernorm_kernel<NV, false, false><<<grid, 256, 0, s>>>(x, ldx, w, b, eps, M, y, ldy, rm);
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
 }
@@ -201,9 +211,13 @@ int launch_hnr(bf16_t* buf, int64_t ld, int col_off, int M, int H, const float* 
 
 }  // namespace
 
-extern "C" int vggt_layernorm(const void* x, int in_dtype, int64_t ldx, const float* w, const float* b, float eps,
-                              int M, int C, void* y, int out_dtype, int64_t ldy, void* stream) {
+extern "C" int vggt_layernorm_grouped(const void* x, int in_dtype, int64_t ldx, const float* w, const float* b,
+                                      float eps, int M, int C, void* y, int out_dtype, int64_t ldy, int group,
+                                      int x_group_stride, int x_row_offset, int y_group_stride, int y_row_offset,
+                                      void* stream) {
   if (M <= 0) return M == 0 ? VGGT_OK : VGGT_ERR_SHAPE;
+  if (group <= 0) return VGGT_ERR_SHAPE;
+  RowMap rm{group, x_group_stride, x_row_offset, y_group_stride, y_row_offset};
   if (C % 256 || C > 4096 || C <= 0) return VGGT_ERR_SHAPE;
   if ((in_dtype != VGGT_DTYPE_F32 && in_dtype != VGGT_DTYPE_BF16) ||
       (out_dtype != VGGT_DTYPE_F32 && out_dtype != VGGT_DTYPE_BF16))
@@ -214,14 +228,20 @@ extern "C" int vggt_layernorm(const void* x, int in_dtype, int64_t ldx, const fl
   hipStream_t s = (hipStream_t)stream;
   const int ib = in_dtype == VGGT_DTYPE_BF16, ob = out_dtype == VGGT_DTYPE_BF16;
   switch (C / 256) {
-    case 1: return launch_ln<1>(x, ib, ldx, w, b, eps, M, y, ob, ldy, s);
-    case 2: return launch_ln<2>(x, ib, ldx, w, b, eps, M, y, ob, ldy, s);
-    case 3: return launch_ln<3>(x, ib, ldx, w, b, eps, M, y, ob, ldy, s);
-    case 4: return launch_ln<4>(x, ib, ldx, w, b, eps, M, y, ob, ldy, s);
-    case 8: return launch_ln<8>(x, ib, ldx, w, b, eps, M, y, ob, ldy, s);
-    case 16: return launch_ln<16>(x, ib, ldx, w, b, eps, M, y, ob, ldy, s);
+    case 1: return launch_ln<1>(x, ib, ldx, w, b, eps, M, y, ob, ldy, rm, s);
+    case 2: return launch_ln<2>(x, ib, ldx, w, b, eps, M, y, ob, ldy, rm, s);
+    case 3: return launch_ln<3>(x, ib, ldx, w, b, eps, M, y, ob, ldy, rm, s);
+    case 4: return launch_ln<4>(x, ib, ldx, w, b, eps, M, y, ob, ldy, rm, s);
+    case 8: return launch_ln<8>(x, ib, ldx, w, b, eps, M, y, ob, ldy, rm, s);
+    case 16: return launch_ln<16>(x, ib, ldx, w, b, eps, M, y, ob, ldy, rm, s);
     default: return VGGT_ERR_SHAPE;
   }
+}
+
+extern "C" int vggt_layernorm(const void* x, int in_dtype, int64_t ldx, const float* w, const float* b, float eps,
+                              int M, int C, void* y, int out_dtype, int64_t ldy, void* stream) {
+  return vggt_layernorm_grouped(x, in_dtype, ldx, w, b, eps, M, C, y, out_dtype, ldy, M > 0 ? M : 1, 0, 0, 0, 0,
+                                stream);
 }
 
 extern "C" int vggt_headnorm_rope(void* buf, int64_t ld, int col_off, int M, int H, int D, const float* w,

@@ -1,0 +1,330 @@
+// Latency-bound pieces of the per-chunk path: skinny fp32 linear layers
+// (camera head trunk, alignment decoder, gated memory update), small-window
+// attention (temporal cross attention with S queries x T keys, decoder and
+// camera-head attention over <= 128 tokens), fp32 QK-norm + RoPE, casts and
+// row-remapped LayerNorm.  See include/vggt_mi355x.h for the contracts.
+#include <math.h>
+
+#include "common.h"
+
+namespace {
+
+// ------------------------------------------------------------------------
+// Skinny fp32 GEMM: out[M,N] = epi(act(A)[M,K] . W[N,K]^T + bias); each
+// block owns a 64-row slab (blockIdx.y) and 64 columns (blockIdx.x).
+// 4 waves per block, each wave owns 16 output columns; K is consumed 16 at a
+// time: every lane loads one float4 of W (row n, k-quad) and of A, and the
+// four v_mfma_f32_16x16x4_f32 of the chunk each take one component (the k
+// order inside a chunk is permuted identically on both operands).
+// Exact f32 products/accumulation (the reference heads run with autocast
+// disabled: featureAligned_vggt.py:104, alignment_head.py:340).
+typedef __attribute__((ext_vector_type(4))) float f4;
+
+template <int ACT_IN, int EPI>
+__global__ __launch_bounds__(256) void linear_f32_kernel(const float* __restrict__ A, int64_t lda,
+                                                         const float* __restrict__ W, int64_t ldw,
+                                                         const float* __restrict__ bias, int M, int N, int K,
+                                                         float* out, int64_t ldo, const float* __restrict__ gamma) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int n0 = (blockIdx.x * 4 + wave) * 16;
+  if (n0 >= N) return;
+  const int mbase = blockIdx.y * 64;
+  A += (int64_t)mbase * lda;
+  out += (int64_t)mbase * ldo;
+  M = min(M - mbase, 64);
+  const int r = lane & 15, q = lane >> 4;
+  const int nrow = min(n0 + r, N - 1);
+  const int mt_n = (M + 15) / 16;
+  f32x4 acc[4] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
+  const bool vec = ((K & 3) == 0) && ((lda & 3) == 0) && ((ldw & 3) == 0);
+  for (int k0 = 0; k0 < K; k0 += 16) {
+    const int kk = k0 + 4 * q;
+    f4 wv;
+    if (vec && kk + 3 < K) {
+      wv = *(const f4*)(W + (int64_t)nrow * ldw + kk);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wv[j] = (kk + j < K) ? W[(int64_t)nrow * ldw + kk + j] : 0.f;
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      if (mt >= mt_n) break;
+      const int m = mt * 16 + r;
+      f4 av = f4{0, 0, 0, 0};
+      if (m < M) {
+        if (vec && kk + 3 < K) {
+          av = *(const f4*)(A + (int64_t)m * lda + kk);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) av[j] = (kk + j < K) ? A[(int64_t)m * lda + kk + j] : 0.f;
+        }
+        if constexpr (ACT_IN == 1) {  // SiLU on the input (poseLN_modulation = Sequential(SiLU, Linear))
+#pragma unroll
+          for (int j = 0; j < 4; ++j) av[j] = av[j] / (1.f + expf(-av[j]));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], wv[j], acc[mt], 0, 0, 0);
+    }
+  }
+  // C[m = 16mt + 4q + i][n = n0 + r]
+  const int n = n0 + r;
+  if (n >= N) return;
+  const float bv = bias ? bias[n] : 0.f;
+  const float g = (EPI == VGGT_EPI_RESID_F32) ? gamma[n] : 0.f;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    if (mt >= mt_n) break;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = mt * 16 + 4 * q + i;
+      if (m >= M) continue;
+      float v = acc[mt][i] + bv;
+      float* op = out + (int64_t)m * ldo + n;
+      if constexpr (EPI == VGGT_EPI_GELU_BF16) v = gelu_erf(v);  // GELU, f32 out
+      if constexpr (EPI == VGGT_EPI_RESID_F32) v = *op + g * v;
+      *op = v;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------
+// Small-window attention: one wave per (group, head); K/V of the group in
+// LDS as f32; keys spread over lanes (<= 2 per lane, nk <= 128), each query
+// row's scores reduced with wave shuffles; output d spread over lanes.
+template <typename T>
+__device__ __forceinline__ float ld1(const T* p) {
+  if constexpr (sizeof(T) == 2) return bf2f(*(const bf16_t*)p);
+  else return *(const float*)p;
+}
+template <typename T>
+__device__ __forceinline__ void st1(T* p, float v) {
+  if constexpr (sizeof(T) == 2) *(bf16_t*)p = f2bf(v);
+  else *(float*)p = v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void attn_small_kernel(const T* __restrict__ q, int64_t ldq, int64_t qbs,
+                                                        const T* __restrict__ k, int64_t ldk, int64_t kbs,
+                                                        const T* __restrict__ v, int64_t ldv, T* __restrict__ o,
+                                                        int64_t ldo, int64_t obs, int heads, int nq, int nk, int D,
+                                                        float scale) {
+  extern __shared__ float sm[];  // Ks[nk][D+1], Vs[nk][D+1], Qr[D]
+  const int lane = threadIdx.x;
+  const int g = blockIdx.x / heads, h = blockIdx.x % heads;
+  const int DP = D + 1;
+  float* Ks = sm;
+  float* Vs = Ks + nk * DP;
+  float* Qr = Vs + nk * DP;
+  const T* kp = k + (int64_t)g * kbs * ldk + h * D;
+  const T* vp = v + (int64_t)g * kbs * ldv + h * D;
+  for (int i = lane; i < nk * D; i += 64) {
+    const int j = i / D, d = i % D;
+    Ks[j * DP + d] = ld1(kp + (int64_t)j * ldk + d);
+    Vs[j * DP + d] = ld1(vp + (int64_t)j * ldv + d);
+  }
+  __syncthreads();
+  for (int qi = 0; qi < nq; ++qi) {
+    const T* qp = q + ((int64_t)g * qbs + qi) * ldq + h * D;
+    for (int d = lane; d < D; d += 64) Qr[d] = ld1(qp + d);
+    __syncthreads();
+    float s0 = -INFINITY, s1 = -INFINITY;
+    if (lane < nk) {
+      float a = 0.f;
+      for (int d = 0; d < D; ++d) a = fmaf(Qr[d], Ks[lane * DP + d], a);
+      s0 = a * scale;
+    }
+    if (lane + 64 < nk) {
+      float a = 0.f;
+      for (int d = 0; d < D; ++d) a = fmaf(Qr[d], Ks[(lane + 64) * DP + d], a);
+      s1 = a * scale;
+    }
+    const float m = wave_max(fmaxf(s0, s1));
+    const float p0 = lane < nk ? expf(s0 - m) : 0.f;
+    const float p1 = lane + 64 < nk ? expf(s1 - m) : 0.f;
+    const float inv = 1.f / wave_sum(p0 + p1);
+    T* op = o + ((int64_t)g * obs + qi) * ldo + h * D;
+    for (int d0 = 0; d0 < D; d0 += 64) {
+      const int d = d0 + lane;
+      float acc = 0.f;
+      for (int j = 0; j < nk; ++j) {
+        const float pj = __shfl(j < 64 ? p0 : p1, j & 63, 64);
+        if (d < D) acc = fmaf(pj, Vs[j * DP + d], acc);
+      }
+      if (d < D) st1(op + d, acc * inv);
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------
+// fp32 per-head LayerNorm + RoPE (decoder / camera head run in fp32).
+template <int MODE>
+__global__ __launch_bounds__(64) void headnorm_rope_f32_kernel(float* __restrict__ buf, int64_t ld, int col_off,
+                                                               int H, int D, const float* __restrict__ w,
+                                                               const float* __restrict__ b, float eps,
+                                                               const int32_t* __restrict__ pos, int period,
+                                                               const float* __restrict__ cs,
+                                                               const float* __restrict__ sn, int tab_len) {
+  extern __shared__ float xs[];
+  const int row = blockIdx.x / H, h = blockIdx.x % H;
+  const int lane = threadIdx.x;
+  float* p = buf + (int64_t)row * ld + col_off + h * D;
+  float s = 0.f;
+  for (int d = lane; d < D; d += 64) {
+    xs[d] = p[d];
+    s += xs[d];
+  }
+  __syncthreads();
+  if (w) {
+    const float mean = wave_sum(s) / D;
+    float qv = 0.f;
+    for (int d = lane; d < D; d += 64) {
+      const float t = xs[d] - mean;
+      qv += t * t;
+    }
+    const float rstd = rsqrtf(wave_sum(qv) / D + eps);
+    __syncthreads();
+    for (int d = lane; d < D; d += 64) xs[d] = (xs[d] - mean) * rstd * w[d] + (b ? b[d] : 0.f);
+    __syncthreads();
+  }
+  for (int d = lane; d < D; d += 64) {
+    float y = xs[d];
+    if constexpr (MODE != VGGT_ROPE_NONE) {
+      const int pr = row % period;
+      int rd, e, pp;
+      if constexpr (MODE == VGGT_ROPE_2D) {
+        rd = D / 2;
+        e = d % rd;
+        pp = pos[2 * pr + (d >= rd ? 1 : 0)];
+      } else {
+        rd = D;
+        e = d;
+        pp = pos[pr];
+      }
+      pp = min(max(pp, 0), tab_len - 1);
+      const int base = d - e;
+      const float partner = e < rd / 2 ? -xs[base + e + rd / 2] : xs[base + e - rd / 2];
+      y = xs[d] * cs[pp * rd + e] + partner * sn[pp * rd + e];
+    }
+    p[d] = y;
+  }
+}
+
+// ------------------------------------------------------------------------
+// fp32 -> bf16 cast of a row-major [rows, cols] view (cols % 4 == 0).
+__global__ __launch_bounds__(256) void cast_kernel(const float* __restrict__ x, int64_t ldx, bf16_t* __restrict__ y,
+                                                   int64_t ldy, int rows, int cols) {
+  const int c4 = cols / 4;
+  const int64_t total = (int64_t)rows * c4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / c4;
+    const int c = (int)(i % c4) * 4;
+    const f32x4 v = *(const f32x4*)(x + r * ldx + c);
+    uint2 u;
+    u.x = pack_bf2(v[0], v[1]);
+    u.y = pack_bf2(v[2], v[3]);
+    *(uint2*)(y + r * ldy + c) = u;
+  }
+}
+
+inline int grid_for(int64_t total) {
+  int64_t g = (total + 255) / 256;
+  return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+}  // namespace
+
+extern "C" int vggt_linear_f32(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, int M,
+                               int N, int K, int act_in, int epi, float* out, int64_t ldo, const float* gamma,
+                               void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return VGGT_ERR_SHAPE;
+  if (epi == VGGT_EPI_RESID_F32 && !gamma) return VGGT_ERR_SHAPE;
+  if ((act_in != 0 && act_in != 1) || (epi != VGGT_EPI_F32 && epi != VGGT_EPI_GELU_BF16 && epi != VGGT_EPI_RESID_F32))
+    return VGGT_ERR_UNSUPPORTED;
+  const dim3 grid((N + 63) / 64, (M + 63) / 64);
+  hipStream_t s = (hipStream_t)stream;
+#define LAUNCH(AI, E) linear_f32_kernel<AI, E><<<grid, 256, 0, s>>>(A, lda, W, ldw, bias, M, N, K, out, ldo, gamma)
+  if (act_in == 0) {
+    if (epi == VGGT_EPI_F32) LAUNCH(0, VGGT_EPI_F32);
+    else if (epi == VGGT_EPI_GELU_BF16) LAUNCH(0, VGGT_EPI_GELU_BF16);
+    else LAUNCH(0, VGGT_EPI_RESID_F32);
+  } else {
+    if (epi == VGGT_EPI_F32) LAUNCH(1, VGGT_EPI_F32);
+    else if (epi == VGGT_EPI_GELU_BF16) LAUNCH(1, VGGT_EPI_GELU_BF16);
+    else LAUNCH(1, VGGT_EPI_RESID_F32);
+  }
+#undef LAUNCH
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+extern "C" int vggt_attention_small(const void* q, int64_t ldq, int64_t q_bstride, const void* k, int64_t ldk,
+                                    int64_t k_bstride, const void* v, int64_t ldv, void* o, int64_t ldo,
+                                    int64_t o_bstride, int dtype, int batch, int heads, int nq, int nk, int D,
+                                    float scale, void* stream) {
+  if (batch <= 0 || heads <= 0 || nq <= 0 || nk <= 0 || nk > 128 || D <= 0 || D > 256) return VGGT_ERR_SHAPE;
+  const size_t lds = (size_t)(2 * nk * (D + 1) + D) * sizeof(float);
+  if (lds > 160 * 1024) return VGGT_ERR_SHAPE;
+  static bool attr_set = false;  // allow > 64 KiB dynamic LDS (gfx950: 160 KiB per workgroup)
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)attn_small_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)attn_small_kernel<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+    attr_set = true;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = batch * heads;
+  if (dtype == VGGT_DTYPE_BF16)
+    attn_small_kernel<bf16_t><<<grid, 64, lds, s>>>((const bf16_t*)q, ldq, q_bstride, (const bf16_t*)k, ldk, k_bstride,
+                                                    (const bf16_t*)v, ldv, (bf16_t*)o, ldo, o_bstride, heads, nq, nk,
+                                                    D, scale);
+  else if (dtype == VGGT_DTYPE_F32)
+    attn_small_kernel<float><<<grid, 64, lds, s>>>((const float*)q, ldq, q_bstride, (const float*)k, ldk, k_bstride,
+                                                   (const float*)v, ldv, (float*)o, ldo, o_bstride, heads, nq, nk, D,
+                                                   scale);
+  else
+    return VGGT_ERR_UNSUPPORTED;
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+extern "C" int vggt_headnorm_rope_f32(float* buf, int64_t ld, int col_off, int M, int H, int D, const float* w,
+                                      const float* b, float eps, int rope_mode, const int32_t* pos, int period,
+                                      const float* cos_tab, const float* sin_tab, int tab_len, void* stream) {
+  if (M <= 0) return M == 0 ? VGGT_OK : VGGT_ERR_SHAPE;
+  if (H <= 0 || D <= 0 || D > 1024 || (D % 4)) return VGGT_ERR_SHAPE;
+  if (rope_mode != VGGT_ROPE_NONE && (!pos || !cos_tab || !sin_tab || period <= 0 || tab_len <= 0))
+    return VGGT_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t lds = D * sizeof(float);
+  const int grid = M * H;
+  switch (rope_mode) {
+    case VGGT_ROPE_NONE:
+      headnorm_rope_f32_kernel<VGGT_ROPE_NONE><<<grid, 64, lds, s>>>(buf, ld, col_off, H, D, w, b, eps, pos, period,
+                                                                    cos_tab, sin_tab, tab_len);
+      break;
+    case VGGT_ROPE_2D:
+      headnorm_rope_f32_kernel<VGGT_ROPE_2D><<<grid, 64, lds, s>>>(buf, ld, col_off, H, D, w, b, eps, pos, period,
+                                                                  cos_tab, sin_tab, tab_len);
+      break;
+    case VGGT_ROPE_1D:
+      headnorm_rope_f32_kernel<VGGT_ROPE_1D><<<grid, 64, lds, s>>>(buf, ld, col_off, H, D, w, b, eps, pos, period,
+                                                                  cos_tab, sin_tab, tab_len);
+      break;
+    default: return VGGT_ERR_UNSUPPORTED;
+  }
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+extern "C" int vggt_cast_f32_bf16(const float* x, int64_t ldx, void* y, int64_t ldy, int rows, int cols,
+                                  void* stream) {
+  if (rows < 0 || cols % 4 || ldx % 4 || ldy % 4) return VGGT_ERR_SHAPE;
+  if (((uintptr_t)x % 16) || ((uintptr_t)y % 8)) return VGGT_ERR_ALIGN;
+  if (rows == 0) return VGGT_OK;
+  cast_kernel<<<grid_for((int64_t)rows * cols / 4), 256, 0, (hipStream_t)stream>>>(x, ldx, (bf16_t*)y, ldy, rows, cols);
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}

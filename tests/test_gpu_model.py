@@ -1,0 +1,101 @@
+"""GPU parity of the full per-chunk FeatureAlignedVGGT forward (aggregator +
+alignment head + camera head + DPT depth/point heads + Sim(3) composition) and
+its multi-chunk ``context`` recurrence against the CPU oracle, through the
+HIP C ABI."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from oracle import vggt_oracle as O  # noqa: E402
+
+
+def _rel(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.fixture(scope="module")
+def models():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from aligned_vggt.models.featureAligned_vggt import FeatureAlignedVGGT
+    from aligned_vggt.utils.synthetic import synthetic_init_
+    m = FeatureAlignedVGGT(enable_point=True, enable_track=False, num_memory_tokens=8)
+    synthetic_init_(m, seed=11)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    return m.cuda().eval(), sd
+
+
+def test_state_dict_names_cover_reference_tree(models):
+    m, sd = models
+    for k in ("aggregator.camera_token", "aggregator.patch_embed.blocks.23.mlp.fc2.weight",
+              "aggregator.global_blocks.23.attn.k_norm.bias", "camera_head.poseLN_modulation.1.weight",
+              "camera_head.trunk.3.ls2.gamma", "depth_head.scratch.refinenet1.resConfUnit1.conv2.weight",
+              "depth_head.resize_layers.3.weight", "depth_head.scratch.output_conv2.2.bias",
+              "alignment_head.temporal_blocks.3.attn.k_norm.weight", "alignment_head.gated_update.gate_mlp.2.bias",
+              "alignment_head.memory_token", "alignment_head.frame_proj.weight", "alignment_head.alpha",
+              "point_head.projects.0.weight"):
+        assert k in sd, k
+
+
+@pytest.mark.parametrize("S,ov,H,W", [(3, 1, 56, 56), (4, 2, 42, 70)])
+def test_feature_aligned_two_chunks(models, S, ov, H, W):
+    m, sd = models
+    from aligned_vggt.utils.synthetic import synthetic_images
+    imgs = synthetic_images(1, 2 * S - ov, H, W, seed=5)
+    chunks = O.generate_chunks(imgs.shape[1], S, ov)
+    ref_ctx = None
+    got_ctx = None
+    for ids in chunks:
+        x = imgs[:, ids]
+        ref_ctx = O.feature_aligned_forward(sd, x, ov, ref_ctx, enable_point=True, bf16=True)
+        got_ctx = m(x.cuda(), ov, got_ctx)
+    torch.cuda.synchronize()
+    r, g = ref_ctx, got_ctx
+    assert len(g["pose_enc"]) == len(chunks)
+    assert g["chunk_sim3_alignment_enc"].shape == r["chunk_sim3_alignment_enc"].shape
+    errs = {
+        "chunk_sim3": _rel(g["chunk_sim3_alignment_enc"], r["chunk_sim3_alignment_enc"]),
+        "frame_se3": _rel(g["frame_se3_alignment_enc"], r["frame_se3_alignment_enc"]),
+        "pose_enc": max(_rel(a, b) for a, b in zip(g["pose_enc"], r["pose_enc"])),
+        "depth": max(_rel(a, b) for a, b in zip(g["depth"], r["depth"])),
+        "depth_conf": max(_rel(a, b) for a, b in zip(g["depth_conf"], r["depth_conf"])),
+        "points": max(_rel(a, b) for a, b in zip(g["world_points"], r["world_points"])),
+        "overlap_tokens": _rel(g["overlap_tokens"], r["overlap_tokens"]),
+        "memory": max(_rel(a, b) for a, b in zip(g["memory_tokens"], r["memory_tokens"])),
+    }
+    print(errs)
+    for k, v in errs.items():
+        assert v < 3e-2, (k, errs)
+
+
+def test_heads_fp32_tier_tight(models):
+    """Camera + depth heads consume the same (oracle-produced) aggregator
+    tokens: both run fp32, so agreement is tight."""
+    m, sd = models
+    from aligned_vggt.utils.synthetic import synthetic_images
+    imgs = synthetic_images(1, 3, 56, 70, seed=9)
+    toks, psi = O.aggregator(sd, imgs, bf16=True)
+    cam_ref = O.camera_head(sd, toks)[-1]
+    d_ref, c_ref = O.dpt_head(sd, "depth_head.", toks, imgs, psi, "exp")
+    tg = [t.cuda() for t in toks]
+    cam = m.camera_head(tg)[-1]
+    d, c = m.depth_head(tg, images=imgs.cuda(), patch_start_idx=psi)
+    assert _rel(cam, cam_ref) < 1e-4
+    assert _rel(d, d_ref) < 1e-4 and _rel(c, c_ref) < 1e-4
+
+
+def test_alignment_head_bf16_tier(models):
+    m, sd = models
+    from aligned_vggt.utils.synthetic import synthetic_images
+    imgs = synthetic_images(1, 4, 42, 56, seed=3)
+    toks, _ = O.aggregator(sd, imgs, bf16=True)
+    ref = O.alignment_head(sd, toks[-1], (42, 56), 2, None, None, bf16=True)
+    got = m.alignment_head(toks[-1].cuda(), (42, 56), 2)
+    for name, a, b in zip(("chunk_sim3", "frame_se3", "memory", "overlap"), got, ref):
+        assert _rel(a, b) < 2e-2, (name, _rel(a, b))
+    ref2 = O.alignment_head(sd, toks[-1], (42, 56), 2, ref[3], ref[2], bf16=True)
+    got2 = m.alignment_head(toks[-1].cuda(), (42, 56), 2, overlap_tokens=ref[3].cuda(), memory_tokens=ref[2].cuda())
+    for name, a, b in zip(("chunk_sim3", "frame_se3", "memory", "overlap"), got2, ref2):
+        assert _rel(a, b) < 2e-2, (name, _rel(a, b))

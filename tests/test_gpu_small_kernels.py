@@ -1,0 +1,184 @@
+"""GPU parity of the fp32 / small-window HIP kernels (heads, decoder) against
+plain PyTorch fp32 references of the same op."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def N():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from aligned_vggt import _native
+    _native.lib()
+    return _native
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("M,Nn,K", [(1, 8, 512), (16, 6144, 2048), (15, 9, 9), (75, 1024, 2048), (23, 100, 36)])
+@pytest.mark.parametrize("epi,act", [(3, 0), (1, 0), (2, 0), (3, 1)])
+def test_linear_f32(N, M, Nn, K, epi, act):
+    g = torch.Generator(device="cuda").manual_seed(M + Nn)
+    a = torch.randn(M, K, device="cuda", generator=g)
+    w = torch.randn(Nn, K, device="cuda", generator=g) / K ** 0.5
+    b = torch.randn(Nn, device="cuda", generator=g)
+    x = F.silu(a) if act else a
+    ref = x @ w.t() + b
+    if epi == 1:
+        ref = F.gelu(ref)
+    out = torch.randn(M, Nn, device="cuda", generator=g)
+    gam = None
+    if epi == 2:
+        gam = torch.rand(Nn, device="cuda", generator=g)
+        ref = out + gam * ref
+    N.linear_f32(a, w, b, out, epi, act_in=act, gamma=gam)
+    assert _rel(out, ref) < 2e-6
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("G,H,nq,nk,D", [(1375, 8, 16, 5, 128), (2, 8, 1, 24, 64), (1, 16, 75, 75, 128),
+                                          (3, 2, 7, 130 - 2, 32)])
+def test_attention_small(N, dt, G, H, nq, nk, D):
+    C = H * D
+    g = torch.Generator(device="cuda").manual_seed(nq * nk)
+    q = torch.randn(G * nq, C, device="cuda", generator=g).to(dt)
+    kv = torch.randn(G * nk, 2 * C, device="cuda", generator=g).to(dt)
+    o = torch.empty(G * nq, C, device="cuda", dtype=dt)
+    N.attention_small(q, kv[:, :C], kv[:, C:], o, G, H, nq, nk, D, nq, nk, nq)
+    qq = q.float().view(G, nq, H, D).transpose(1, 2)
+    kk = kv[:, :C].float().view(G, nk, H, D).transpose(1, 2)
+    vv = kv[:, C:].float().view(G, nk, H, D).transpose(1, 2)
+    ref = torch.softmax(qq @ kk.transpose(-1, -2) * D ** -0.5, -1) @ vv
+    ref = ref.transpose(1, 2).reshape(G * nq, C)
+    assert _rel(o, ref) < (4e-3 if dt == torch.bfloat16 else 1e-5)
+
+
+def test_headnorm_rope_f32_matches_oracle(N):
+    from oracle import vggt_oracle as O
+    from aligned_vggt.layers.rope import RotaryPositionEmbedding
+    H, D, M = 8, 64, 24
+    x = torch.randn(M, H * D)
+    w, b = torch.randn(D), torch.randn(D)
+    pos = torch.arange(M) * 2
+    cos, sin = RotaryPositionEmbedding().tables(D, int(pos.max()), "cuda")
+    buf = x.clone().cuda()
+    N.headnorm_rope_any(buf, 0, H, D, w.cuda(), b.cuda(), 1e-5, N.ROPE_1D, pos.to(torch.int32).cuda(), M, cos, sin)
+    ref = O.rope1d(O.layer_norm(x.view(M, H, D).transpose(0, 1)[None], w, b, 1e-5), pos[None])
+    ref = ref[0].transpose(0, 1).reshape(M, H * D)
+    assert _rel(buf.cpu(), ref) < 1e-6
+
+
+def test_rope_module_matches_reference_fixture(N, golden):
+    from aligned_vggt.layers.rope import RotaryPositionEmbedding
+    g = golden("rope1d")
+    for i in range(3):
+        y = RotaryPositionEmbedding()(torch.from_numpy(g[f"x{i}"]).cuda(), torch.from_numpy(g[f"pos{i}"]).cuda())
+        torch.testing.assert_close(y.cpu(), torch.from_numpy(g[f"y{i}"]), atol=2e-6, rtol=0)
+
+
+def test_gated_update_matches_reference_fixture(N, golden):
+    from aligned_vggt.layers.gated_update import GatedUpdate
+    for tag in ("d64", "d32"):
+        g = golden("gated_update_" + tag)
+        D, Nt = g["memory"].shape[2], g["memory"].shape[1]
+        m = GatedUpdate(D, Nt)
+        m.load_state_dict({k[2:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("p.")})
+        m = m.cuda()
+        out = m(torch.from_numpy(g["memory"]).cuda(), torch.from_numpy(g["update"]).cuda())
+        torch.testing.assert_close(out.cpu(), torch.from_numpy(g["out"]), atol=2e-5, rtol=0)
+
+
+def test_layernorm_grouped_and_cast(N):
+    F_, P, C, skip = 3, 21, 1024, 5
+    x = torch.randn(F_ * P, C, device="cuda")
+    w, b = torch.randn(C, device="cuda"), torch.randn(C, device="cuda")
+    hw = P - skip
+    y = torch.zeros(F_ * hw, C, device="cuda")
+    N.layernorm_grouped(x, w, b, 1e-5, y, F_ * hw, C, hw, P, skip, hw, 0)
+    ref = F.layer_norm(x.view(F_, P, C)[:, skip:], (C,), w, b, 1e-5).reshape(-1, C)
+    assert _rel(y, ref) < 1e-6
+    z = torch.zeros(F_ * (hw + 1), C, device="cuda")
+    N.layernorm_grouped(y, w, b, 1e-5, z, F_ * hw, C, hw, hw, 0, hw + 1, 1)
+    assert z.view(F_, hw + 1, C)[:, 0].abs().max() == 0
+    xb = torch.empty(F_ * P, C, device="cuda", dtype=torch.bfloat16)
+    N.cast_f32_bf16(x, xb)
+    assert torch.equal(xb, x.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("case", ["3x3", "3x3s2", "1x1pos", "rcu", "shuffle4", "shuffle2", "co2"])
+def test_conv2d_f32(N, case):
+    g = torch.Generator(device="cuda").manual_seed(hash(case) % 1000)
+    n, hi, wi = 2, 13, 11
+    ci, co, k, s, p = 64, 64, 3, 1, 1
+    if case == "3x3s2":
+        s = 2
+    if case == "1x1pos":
+        k, p, co = 1, 0, 128
+    if case == "co2":
+        k, p, ci, co = 1, 0, 32, 2
+    if case.startswith("shuffle"):
+        f = int(case[-1])
+        x = torch.randn(n, ci, hi, wi, device="cuda", generator=g)
+        wt = torch.randn(ci, co, f, f, device="cuda", generator=g) / ci ** 0.5
+        bt = torch.randn(co, device="cuda", generator=g)
+        ref = F.conv_transpose2d(x, wt, bt, stride=f)
+        wp = wt.permute(2, 3, 1, 0).reshape(f * f * co, ci)
+        wp = torch.cat([wp, wp.new_zeros((-wp.shape[0]) % 64, ci)])
+        xr = x.permute(0, 2, 3, 1).reshape(-1, ci).contiguous()
+        y = torch.empty(n * hi * f * wi * f, co, device="cuda")
+        N.conv2d_f32(xr, n, hi, wi, ci, wp.contiguous(), bt, co, 1, 1, 1, 0, y, shuffle=f)
+        got = y.view(n, hi * f, wi * f, co).permute(0, 3, 1, 2)
+        assert _rel(got, ref) < 2e-6
+        return
+    x = torch.randn(n, ci, hi, wi, device="cuda", generator=g)
+    w = torch.randn(co, ci, k, k, device="cuda", generator=g) / (ci * k * k) ** 0.5
+    b = torch.randn(co, device="cuda", generator=g)
+    ho, wo = (hi + 2 * p - k) // s + 1, (wi + 2 * p - k) // s + 1
+    xr = x.permute(0, 2, 3, 1).reshape(-1, ci).contiguous()
+    wp = w.permute(0, 2, 3, 1).reshape(co, -1)
+    wp = torch.cat([wp, wp.new_zeros((-co) % 64, wp.shape[1])]).contiguous()
+    y = torch.empty(n * ho * wo, co, device="cuda")
+    kw = {}
+    ref_in = x
+    if case == "rcu":
+        kw = dict(relu_in=True, relu_out=True)
+        ref_in = F.relu(x)
+    pos = None
+    if case == "1x1pos":
+        pos = torch.randn(ho * wo, co, device="cuda", generator=g)
+    r1 = r2 = None
+    if case == "3x3":
+        r1 = torch.randn(n * ho * wo, co, device="cuda", generator=g)
+        r2 = torch.randn(n * ho * wo, co, device="cuda", generator=g)
+    N.conv2d_f32(xr, n, hi, wi, ci, wp, b, co, k, k, s, p, y, res1=r1, res1_relu=True, res2=r2, pos=pos, **kw)
+    ref = F.conv2d(ref_in, w, b, stride=s, padding=p)
+    if case == "rcu":
+        ref = F.relu(ref)
+    ref = ref.permute(0, 2, 3, 1).reshape(-1, co)
+    if pos is not None:
+        ref = ref + pos.repeat(n, 1)
+    if r1 is not None:
+        ref = ref + F.relu(r1) + r2
+    assert _rel(y, ref) < 2e-6
+
+
+def test_upsample_and_activate(N):
+    n, hi, wi, C = 2, 7, 9, 8
+    x = torch.randn(n, C, hi, wi, device="cuda")
+    ref = F.interpolate(x, size=(20, 13), mode="bilinear", align_corners=True)
+    y = torch.empty(n * 20 * 13, C, device="cuda")
+    N.upsample_bilinear_f32(x.permute(0, 2, 3, 1).reshape(-1, C).contiguous(), n, hi, wi, C, y, 20, 13)
+    assert _rel(y.view(n, 20, 13, C).permute(0, 3, 1, 2), ref) < 1e-6
+    z = torch.randn(100, 4, device="cuda")
+    pts = torch.empty(100, 3, device="cuda")
+    conf = torch.empty(100, device="cuda")
+    sc = torch.tensor([2.0, 3.0], device="cuda")
+    N.dpt_activate(z, 100, 50, 4, 1, sc, pts, conf)
+    ref = torch.sign(z[:, :3]) * torch.expm1(z[:, :3].abs()) * sc.repeat_interleave(50)[:, None]
+    assert _rel(pts, ref) < 1e-6
+    assert _rel(conf, 1 + z[:, 3].exp()) < 1e-6
