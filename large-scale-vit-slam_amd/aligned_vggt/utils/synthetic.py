@@ -38,3 +38,28 @@ def synthetic_images(B: int, S: int, H: int, W: int, seed: int = 1234, device="c
     """Uniform [0, 1) frames (B,S,3,H,W), generator seed 1234."""
     g = torch.Generator().manual_seed(seed)
     return torch.rand(B, S, 3, H, W, generator=g).to(device)
+
+
+@torch.no_grad()
+def condition_pose_outputs_(model: nn.Module) -> nn.Module:
+    """Put the random-init pose decoders in a well-conditioned regime.
+
+    With N(0, 0.02) weights the camera head / alignment decoders emit
+    quaternions of norm ~1e-2, whose direction (all the reference uses:
+    quaternions are normalised before use, data.py:45, rotation.quat_to_mat)
+    is then ill-conditioned.  Trained models emit near-unit quaternions; we
+    emulate that by biasing the last decoder layers towards the identity
+    rotation and a ~1 rad field of view.  Only biases change."""
+    cam = getattr(model, "camera_head", None)
+    if cam is not None:
+        b = cam.pose_branch.fc2.bias
+        b.zero_()
+        b[6] = 0.25  # quat w, accumulated over 4 refinement iterations
+        b[7:9] = 0.25  # FoV (h, w) -> ~1 rad after 4 iterations
+    ah = getattr(model, "alignment_head", None)
+    if ah is not None:
+        for dec in (ah.chunk_sim3_decoder, ah.frame_se3_decoder):
+            b = dec.fc2.bias
+            b.zero_()
+            b[6] = 1.0
+    return model

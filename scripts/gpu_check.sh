@@ -12,6 +12,7 @@ export TMPDIR=/tmp
 step() { local name=$1; shift; local t=$1; shift; echo "[$(date +%T)] $name ..."; timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1; local rc=$?; echo "[$(date +%T)] $name rc=$rc"; tail -n 5 "$OUT/$name.log"; return $rc; }
 step pytest 1200 python -m pytest tests -m gpu -q -rf "$@"; rc=$?
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping: pytest rc=$rc"; exit $rc; fi
+[ -n "${SKIP_BENCH:-}" ] && { echo "bench skipped"; exit 0; }
 step bench 900 python bench.py --steps 5 --warmup 2 || exit $?
 step prof 900 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof" -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit $?
 echo done

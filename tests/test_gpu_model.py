@@ -20,9 +20,10 @@ def models():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     from aligned_vggt.models.featureAligned_vggt import FeatureAlignedVGGT
-    from aligned_vggt.utils.synthetic import synthetic_init_
+    from aligned_vggt.utils.synthetic import condition_pose_outputs_, synthetic_init_
     m = FeatureAlignedVGGT(enable_point=True, enable_track=False, num_memory_tokens=8)
     synthetic_init_(m, seed=11)
+    condition_pose_outputs_(m)
     sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
     return m.cuda().eval(), sd
 
@@ -45,29 +46,39 @@ def test_feature_aligned_two_chunks(models, S, ov, H, W):
     from aligned_vggt.utils.synthetic import synthetic_images
     imgs = synthetic_images(1, 2 * S - ov, H, W, seed=5)
     chunks = O.generate_chunks(imgs.shape[1], S, ov)
-    ref_ctx = None
+    ref_ctx = ref32 = None
     got_ctx = None
     for ids in chunks:
         x = imgs[:, ids]
         ref_ctx = O.feature_aligned_forward(sd, x, ov, ref_ctx, enable_point=True, bf16=True)
+        ref32 = O.feature_aligned_forward(sd, x, ov, ref32, enable_point=True, bf16=False)
         got_ctx = m(x.cuda(), ov, got_ctx)
     torch.cuda.synchronize()
+
+    def errs(g, r):
+        return {
+            "chunk_sim3": _rel(g["chunk_sim3_alignment_enc"], r["chunk_sim3_alignment_enc"]),
+            "frame_se3": _rel(g["frame_se3_alignment_enc"], r["frame_se3_alignment_enc"]),
+            "pose_enc": max(_rel(a, b) for a, b in zip(g["pose_enc"], r["pose_enc"])),
+            "depth": max(_rel(a, b) for a, b in zip(g["depth"], r["depth"])),
+            "depth_conf": max(_rel(a, b) for a, b in zip(g["depth_conf"], r["depth_conf"])),
+            "points": max(_rel(a, b) for a, b in zip(g["world_points"], r["world_points"])),
+            "overlap_tokens": _rel(g["overlap_tokens"], r["overlap_tokens"]),
+            "memory": max(_rel(a, b) for a, b in zip(g["memory_tokens"], r["memory_tokens"])),
+        }
     r, g = ref_ctx, got_ctx
     assert len(g["pose_enc"]) == len(chunks)
     assert g["chunk_sim3_alignment_enc"].shape == r["chunk_sim3_alignment_enc"].shape
-    errs = {
-        "chunk_sim3": _rel(g["chunk_sim3_alignment_enc"], r["chunk_sim3_alignment_enc"]),
-        "frame_se3": _rel(g["frame_se3_alignment_enc"], r["frame_se3_alignment_enc"]),
-        "pose_enc": max(_rel(a, b) for a, b in zip(g["pose_enc"], r["pose_enc"])),
-        "depth": max(_rel(a, b) for a, b in zip(g["depth"], r["depth"])),
-        "depth_conf": max(_rel(a, b) for a, b in zip(g["depth_conf"], r["depth_conf"])),
-        "points": max(_rel(a, b) for a, b in zip(g["world_points"], r["world_points"])),
-        "overlap_tokens": _rel(g["overlap_tokens"], r["overlap_tokens"]),
-        "memory": max(_rel(a, b) for a, b in zip(g["memory_tokens"], r["memory_tokens"])),
-    }
-    print(errs)
-    for k, v in errs.items():
-        assert v < 3e-2, (k, errs)
+    e_hip = errs(g, r)            # HIP vs bf16-mixed reference emulation
+    e_ref = errs(ref32, r)        # the reference's own bf16-vs-fp32 spread
+    print("hip", e_hip)
+    print("ref bf16 vs fp32", e_ref)
+    # North-star tolerance on the Sim(3) alignment outputs: 1e-3 relative.
+    assert e_hip["chunk_sim3"] < 1e-3, e_hip
+    # Everything else: within 3e-2, or within the reference's own mixed-precision
+    # spread (random-init camera/decoder weights amplify token-level rounding).
+    for k, v in e_hip.items():
+        assert v < max(3e-2, 1.5 * e_ref[k]), (k, e_hip, e_ref)
 
 
 def test_heads_fp32_tier_tight(models):
@@ -99,3 +110,34 @@ def test_alignment_head_bf16_tier(models):
     got2 = m.alignment_head(toks[-1].cuda(), (42, 56), 2, overlap_tokens=ref[3].cuda(), memory_tokens=ref[2].cuda())
     for name, a, b in zip(("chunk_sim3", "frame_se3", "memory", "overlap"), got2, ref2):
         assert _rel(a, b) < 2e-2, (name, _rel(a, b))
+
+
+def test_feature_aligned_given_oracle_tokens(models, monkeypatch):
+    """Feed the oracle's aggregator tokens into the HIP model: isolates the
+    alignment head + heads + Sim(3) composition (per-component report)."""
+    m, sd = models
+    from aligned_vggt.utils.synthetic import synthetic_images
+    S, ov, H, W = 4, 2, 42, 70
+    imgs = synthetic_images(1, 2 * S - ov, H, W, seed=5)
+    chunks = O.generate_chunks(imgs.shape[1], S, ov)
+    ref_ctx = got_ctx = None
+    for ids in chunks:
+        x = imgs[:, ids]
+        toks, psi = O.aggregator(sd, x, bf16=True)
+        monkeypatch.setattr(m.aggregator, "forward", lambda images, keep_layers=None, t=toks: ([a.cuda() for a in t], 5))
+        ref_ctx = O.feature_aligned_forward(sd, x, ov, ref_ctx, enable_point=True, bf16=True)
+        got_ctx = m(x.cuda(), ov, got_ctx)
+    for ci, (a, b) in enumerate(zip(got_ctx["pose_enc"], ref_ctx["pose_enc"])):
+        a = a.cpu()
+        print("chunk", ci, "T", _rel(a[..., :3], b[..., :3]), "quat", _rel(a[..., 3:7], b[..., 3:7]),
+              "fov", _rel(a[..., 7:], b[..., 7:]))
+        print("  got", a[0, :, :7])
+        print("  ref", b[0, :, :7])
+    print("sim3", _rel(got_ctx["chunk_sim3_alignment_enc"], ref_ctx["chunk_sim3_alignment_enc"]))
+    for a, b in zip(got_ctx["pose_enc"], ref_ctx["pose_enc"]):
+        assert _rel(a[..., 7:], b[..., 7:]) < 1e-5
+        assert _rel(a[..., 3:7], b[..., 3:7]) < 2e-3
+        assert _rel(a[..., :3], b[..., :3]) < 5e-3
+    assert _rel(got_ctx["chunk_sim3_alignment_enc"], ref_ctx["chunk_sim3_alignment_enc"]) < 1e-3
+    for a, b in zip(got_ctx["depth"], ref_ctx["depth"]):
+        assert _rel(a, b) < 1e-3
