@@ -112,7 +112,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="aggregator", choices=["aggregator"])
+    ap.add_argument("--workload", default="aggregator", choices=["aggregator", "chunk", "sequence"],
+                    help="aggregator: BASELINE configs[1] headline (default); chunk: full FeatureAlignedVGGT "
+                         "per-chunk forward (encoder + alignment head + camera/depth heads); sequence: configs[2..4] "
+                         "chunk pipeline over --seq-frames frames (RCCL baton ring at N>1)")
+    ap.add_argument("--seq-frames", type=int, default=64)
+    ap.add_argument("--height", type=int, default=H_IMG)
+    ap.add_argument("--overlap", type=int, default=4)
     ap.add_argument("--frames", type=int, default=S_FRAMES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
@@ -131,6 +137,9 @@ def main():
     from aligned_vggt import _native
     from aligned_vggt.backbone.aggregator import Aggregator
     from aligned_vggt.utils.synthetic import synthetic_images, synthetic_init_
+
+    if args.workload != "aggregator":
+        return bench_full(args, world, rank, dev)
 
     agg = Aggregator().to(dev)
     synthetic_init_(agg, seed=0)
@@ -204,6 +213,68 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_full(args, world, rank, dev):
+    """Full per-chunk model (configs[2..4]): 'chunk' = one FeatureAlignedVGGT
+    forward per rank per step (context threaded step to step); 'sequence' =
+    one ChunkPipeline pass over a synthetic --seq-frames sequence per step."""
+    import torch.distributed as dist
+    from aligned_vggt.dist.pipeline import ChunkPipeline
+    from aligned_vggt.models.featureAligned_vggt import FeatureAlignedVGGT
+    from aligned_vggt.utils.data import generate_chunks
+    from aligned_vggt.utils.synthetic import condition_pose_outputs_, synthetic_images, synthetic_init_
+    model = FeatureAlignedVGGT(enable_point=False, enable_track=False, num_memory_tokens=8).to(dev).eval()
+    synthetic_init_(model, seed=0)
+    condition_pose_outputs_(model)
+    H, W = args.height, W_IMG
+    S, ov = args.frames, args.overlap
+    if args.workload == "chunk":
+        imgs = synthetic_images(1, S, H, W, seed=1234 + rank, device=dev)
+        ctx = {"c": None}
+
+        def step():
+            ctx["c"] = model(imgs, ov, ctx["c"])
+            for k in ("depth", "depth_conf", "images", "pose_enc", "memory_tokens"):
+                if k in ctx["c"] and isinstance(ctx["c"][k], list) and len(ctx["c"][k]) > 2:
+                    del ctx["c"][k][0]
+        n_chunks_step = world
+    else:
+        seq = synthetic_images(1, args.seq_frames, H, W, seed=1234, device="cpu")
+        pipe = ChunkPipeline(model, device=dev)
+        P1 = 6 + (H // 14) * (W // 14)
+
+        def step():
+            pipe.run(seq, S, ov, token_dims=(P1, 1024), memory_shape=(1, 8, 512))
+        n_chunks_step = len(generate_chunks(args.seq_frames, "chunk_overlap", S, ov))
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+        dist.destroy_process_group()
+    if rank == 0:
+        value = n_chunks_step * args.steps / dt
+        print(json.dumps({
+            "metric": "chunks/sec (%d-frame %dx%d) full per-chunk FeatureAlignedVGGT" % (S, H, W),
+            "value": round(value, 4), "unit": "chunks/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak" if args.workload == "chunk" else "strong", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic", "config": {"workload": args.workload, "frames": S, "overlap": ov,
+                                            "seq_frames": args.seq_frames if args.workload == "sequence" else None,
+                                            "image": [H, W], "heads": "camera+depth+alignment(memory 8)"}}),
+              flush=True)
 
 
 if __name__ == "__main__":

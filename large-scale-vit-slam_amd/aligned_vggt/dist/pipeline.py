@@ -1,0 +1,191 @@
+"""Sequence drivers: the reference's single-process chunk loop and a
+multi-GPU chunk pipeline.
+
+``apply_sequence_to_model`` restates training_metrics.py:616-659: chunk the
+sequence (data.py:155), run the model chunk by chunk threading ``context``,
+offload older chunk outputs to host memory, merge the per-chunk lists with
+overlap removal (data.py:54-87).
+
+``ChunkPipeline`` is the MI355X-native multi-GPU form (one process per GPU,
+torch.distributed; backend "nccl" = RCCL over xGMI on ROCm, "gloo" for CPU
+tests).  The per-chunk work splits into
+
+  * ``encode_chunk``: aggregator + camera/depth/point heads -- ~99% of the
+    FLOPs and independent of every other chunk; chunk i is encoded on rank
+    i % world, all ranks in parallel;
+  * ``align_chunk``: alignment head + Sim(3) composition -- a strict
+    recurrence (chunk i consumes chunk i-1's post-head overlap tokens, memory
+    tokens and aligned poses, featureAligned_vggt.py:88-90,126).
+
+The recurrence state (the "baton": overlap tokens (B, ov+1, P+1, 1024) fp32
+~28 MB, memory (B, 8, 512), last pose encoding (B, S, 9)) travels rank to rank
+with point-to-point send/recv: one hop per chunk boundary over one xGMI link
+(~0.2 ms), hidden behind the next chunk's encode.  Each rank interleaves
+encode(own chunk k) -> align(own chunk k) so that, with align << encode, the
+baton ring never stalls an encode.  At the end the small per-chunk outputs
+(pose encodings, Sim(3)/SE(3) alignments) are all-gathered; dense maps (depth,
+points) stay on the rank that produced them unless ``gather_dense``.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..utils.data import chunk_batch, convertDictListsToTensors, generate_chunks, moveDictListItemToCPU
+
+
+def apply_sequence_to_model(batch: dict, model, chunk_width, num_overlap, sample_mode: str = "chunk_overlap",
+                            alignment_type: Optional[str] = None) -> dict:
+    """training_metrics.py:616-659 (no_grad inference chunk loop)."""
+    S = batch["images"].shape[1]
+    chunk_width = chunk_width[0] if isinstance(chunk_width, (list, tuple)) else chunk_width
+    num_overlap = num_overlap[0] if isinstance(num_overlap, (list, tuple)) else num_overlap
+    indices = generate_chunks(S, sample_mode, chunk_width, num_overlap)
+    chunked = chunk_batch(batch, indices)
+    preds = None
+    for i in range(len(indices)):
+        gt = chunked["extrinsics"][i] if sample_mode in ("chunk_gt", "two_chunks") and "extrinsics" in chunked else None
+        with torch.no_grad():
+            preds = model(chunked["images"][i], num_overlap, preds, gt_poses=gt)
+        moveDictListItemToCPU(preds, -2)
+    moveDictListItemToCPU(preds, -1)
+    if alignment_type not in (None, "null", "none"):
+        raise NotImplementedError("GT-based output alignment (data.py:108-153) is evaluation post-processing, "
+                                  "out of scope for the hot path (SURVEY.md §2)")
+    out = {}
+    convertDictListsToTensors(preds, num_overlap if len(indices) > 1 else 0, out)
+    for k in ("chunk_sim3_alignment_enc", "frame_se3_alignment_enc"):
+        if k in preds:
+            out[k] = preds[k]
+    return out
+
+
+def _overlap_of(S: int, num_overlap: int) -> int:
+    """featureAligned_vggt.py:93."""
+    return num_overlap if S > num_overlap else S - 1
+
+
+class ChunkPipeline:
+    """Run a whole sequence through ``model`` with chunks spread over the
+    ranks of ``group`` (see module docstring).  ``model`` must provide
+    ``encode_chunk(images)`` and ``align_chunk(enc, num_overlap, context)``
+    (FeatureAlignedVGGT does) and be replicated on every rank."""
+
+    def __init__(self, model, group=None, device=None, gather_dense: bool = False):
+        self.model = model
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.device = device
+        self.gather_dense = gather_dense
+
+    # ---------------------------------------------------------- baton I/O
+    def _baton_shapes(self, B: int, S_prev: int, ov_prev: int, P1: int, C: int, mem):
+        shapes = {"overlap_tokens": (B, ov_prev + 1, P1, C), "pose_enc": (B, S_prev, 9)}
+        if mem is not None:
+            shapes["memory_tokens"] = mem
+        return shapes
+
+    def _send(self, ctx: dict, dst: int, keys):
+        for k in keys:
+            t = ctx[k][-1] if isinstance(ctx[k], list) else ctx[k]
+            dist.send(t.contiguous().to(self.device), dst, group=self.group)
+
+    def _recv(self, src: int, shapes: Dict[str, tuple]) -> dict:
+        out = {}
+        for k, shp in shapes.items():
+            t = torch.empty(shp, device=self.device, dtype=torch.float32)
+            dist.recv(t, src, group=self.group)
+            out[k] = t
+        return out
+
+    # ---------------------------------------------------------------- run
+    @torch.no_grad()
+    def run(self, images: torch.Tensor, chunk_width: int, num_overlap: int, token_dims=None,
+            memory_shape=None) -> Optional[dict]:
+        """images: (B, N, 3, H, W) (any device; each rank moves only its
+        chunks).  token_dims = (P+1, C) of the alignment head's tokens;
+        memory_shape = (B, n_mem, dec) or None.  Returns merged predictions on
+        rank 0 (pose_enc (B,N,9), chunk_sim3_alignment_enc (B,n_chunks,8),
+        frame_se3_alignment_enc (B,sum(S_i-1),7), and depth/points if gathered),
+        None elsewhere."""
+        B, Nf = images.shape[:2]
+        chunks = generate_chunks(Nf, "chunk_overlap", chunk_width, num_overlap)
+        n = len(chunks)
+        W, r = self.world, self.rank
+        P1, C = token_dims
+        keys = ["overlap_tokens", "pose_enc"] + (["memory_tokens"] if memory_shape is not None else [])
+        mine: Dict[int, dict] = {}
+        local = None  # baton kept in memory when the next chunk stays on this rank (W == 1)
+        for i in range(r, n, W):
+            x = images[:, chunks[i]].to(self.device)
+            enc = self.model.encode_chunk(x)
+            ctx = None
+            if i > 0:
+                Sp = len(chunks[i - 1])
+                if W == 1:
+                    ctx_in = local
+                else:
+                    ctx_in = self._recv((i - 1) % W, self._baton_shapes(B, Sp, _overlap_of(Sp, num_overlap), P1, C,
+                                                                       memory_shape))
+                ctx = {"overlap_tokens": ctx_in["overlap_tokens"], "pose_enc": [ctx_in["pose_enc"]],
+                       "chunk_sim3_alignment_enc": torch.zeros(B, 0, 8, device=self.device),
+                       "frame_se3_alignment_enc": torch.zeros(B, 0, 7, device=self.device)}
+                if memory_shape is not None:
+                    ctx["memory_tokens"] = [ctx_in["memory_tokens"]]
+            pred = self.model.align_chunk(enc, num_overlap, ctx)
+            if i + 1 < n:
+                if W == 1:
+                    local = {k: (pred[k][-1] if isinstance(pred[k], list) else pred[k]) for k in keys}
+                else:
+                    self._send(pred, (i + 1) % W, keys)
+            mine[i] = {"pose_enc": pred["pose_enc"][-1], "chunk_sim3": pred["chunk_sim3_alignment_enc"][:, -1:],
+                       "frame_se3": pred["frame_se3_alignment_enc"][:, -(len(chunks[i]) - 1):]
+                       if len(chunks[i]) > 1 else pred["frame_se3_alignment_enc"][:, :0]}
+            if "depth" in pred:
+                mine[i]["depth"] = pred["depth"][-1]
+                mine[i]["depth_conf"] = pred["depth_conf"][-1]
+        return self._gather(mine, chunks, num_overlap, B)
+
+    def _gather(self, mine: Dict[int, dict], chunks: List[List[int]], num_overlap: int, B: int) -> Optional[dict]:
+        n = len(chunks)
+        W = self.world
+        dense = self.gather_dense and any("depth" in v for v in mine.values())
+        if W > 1:
+            # every chunk's small outputs -> rank 0 (fixed, known shapes)
+            per_chunk = {}
+            for i in range(n):
+                owner = i % W
+                S = len(chunks[i])
+                shp = {"pose_enc": (B, S, 9), "chunk_sim3": (B, 1, 8), "frame_se3": (B, S - 1, 7)}
+                if dense:
+                    H, Wd = next(iter(mine.values()))["depth"].shape[2:4] if mine else (0, 0)
+                    shp["depth"] = (B, S, H, Wd, 1)
+                    shp["depth_conf"] = (B, S, H, Wd)
+                if owner == self.rank and self.rank == 0:
+                    per_chunk[i] = mine[i]
+                elif owner == self.rank:
+                    for k in shp:
+                        dist.send(mine[i][k].contiguous().to(self.device), 0, group=self.group)
+                elif self.rank == 0:
+                    per_chunk[i] = {}
+                    for k, s in shp.items():
+                        t = torch.empty(s, device=self.device)
+                        dist.recv(t, owner, group=self.group)
+                        per_chunk[i][k] = t
+            if self.rank != 0:
+                return None
+        else:
+            per_chunk = mine
+        ov = num_overlap
+        out = {
+            "pose_enc": torch.cat([per_chunk[i]["pose_enc"][:, (ov if i > 0 else 0):] for i in range(n)], 1),
+            "chunk_sim3_alignment_enc": torch.cat([per_chunk[i]["chunk_sim3"] for i in range(n)], 1),
+            "frame_se3_alignment_enc": torch.cat([per_chunk[i]["frame_se3"] for i in range(n)], 1),
+        }
+        if all("depth" in per_chunk[i] for i in range(n)):
+            out["depth"] = torch.cat([per_chunk[i]["depth"][:, (ov if i > 0 else 0):] for i in range(n)], 1)
+            out["depth_conf"] = torch.cat([per_chunk[i]["depth_conf"][:, (ov if i > 0 else 0):] for i in range(n)], 1)
+        return out

@@ -64,10 +64,33 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
 
     @torch.no_grad()
     def forward(self, images: torch.Tensor, num_overlap: int, context: dict = None, gt_poses: torch.Tensor = None) -> dict:
+        """featureAligned_vggt.py:48-225.  Split into the context-free
+        :meth:`encode_chunk` (aggregator + camera/depth/point heads: ~99% of
+        the FLOPs, embarrassingly parallel over chunks) and the recurrent
+        :meth:`align_chunk` (alignment head + Sim(3)/SE(3) composition), so the
+        multi-GPU pipeline (aligned_vggt.dist) can run encodes ahead of the
+        alignment baton.  forward == align_chunk(encode_chunk(.)) exactly."""
+        return self.align_chunk(self.encode_chunk(images), num_overlap, context, gt_poses)
+
+    @torch.no_grad()
+    def encode_chunk(self, images: torch.Tensor) -> dict:
+        B, S, C, H, W = images.shape
+        toks, patch_start_idx = self.aggregator(images, keep_layers=self.intermediate_layer_indices)
+        enc = {"images": images, "tokens": toks, "patch_start_idx": patch_start_idx}
+        if self.camera_head is not None:
+            enc["cam_pose_enc"] = self.camera_head(toks)[-1]
+        if self.depth_head is not None:
+            enc["depth"], enc["depth_conf"] = self.depth_head(toks, images=images, patch_start_idx=patch_start_idx)
+        if self.point_head is not None:
+            enc["points"], enc["points_conf"] = self.point_head(toks, images=images, patch_start_idx=patch_start_idx)
+        return enc
+
+    @torch.no_grad()
+    def align_chunk(self, enc: dict, num_overlap: int, context: dict = None, gt_poses: torch.Tensor = None) -> dict:
+        images = enc["images"]
+        toks = enc["tokens"]
         B, S, C, H, W = images.shape
         predictions = {}
-        toks, patch_start_idx = self.aggregator(images, keep_layers=self.intermediate_layer_indices)
-
         ctx_overlap = ctx_memory = None
         if context is not None:
             ctx_overlap = context["overlap_tokens"]
@@ -84,8 +107,7 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
 
         point_identity_alignment = None
         if self.camera_head is not None:
-            pose_enc_list = self.camera_head(toks)
-            extr, intr = pose_encoding_to_extri_intri(pose_enc_list[-1], image_size_hw=images.shape[-2:])
+            extr, intr = pose_encoding_to_extri_intri(enc["cam_pose_enc"], image_size_hw=images.shape[-2:])
             extr = F.pad(extr, (0, 0, 0, 1, 0, 0, 0, 0), mode="constant")
             extr[:, :, 3, 3] = 1.0
             ident = closed_form_inverse_se3(extr[:, 0])
@@ -130,8 +152,8 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
                     predictions["memory_tokens"] = context["memory_tokens"]
 
         if self.depth_head is not None:
-            depth, depth_conf = self.depth_head(toks, images=images, patch_start_idx=patch_start_idx,
-                                                _scale=chunk_scale.reshape(B))
+            depth = enc["depth"] * chunk_scale.view(B, 1, 1, 1, 1)
+            depth_conf = enc["depth_conf"]
             if context is None:
                 predictions["depth"] = [depth]
                 predictions["depth_conf"] = [depth_conf]
@@ -142,7 +164,7 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
                 predictions["depth_conf"] = context["depth_conf"]
 
         if self.point_head is not None:
-            pts3d, pts3d_conf = self.point_head(toks, images=images, patch_start_idx=patch_start_idx)
+            pts3d, pts3d_conf = enc["points"], enc["points_conf"]
             if self.camera_head is not None:
                 if context is not None:
                     pt = closed_form_inverse_se3(per_frame_se3[:, 0]).unsqueeze(1)
