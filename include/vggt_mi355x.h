@@ -84,6 +84,16 @@ int vggt_headnorm_rope(void* buf, int64_t ld, int col_off, int M, int H, int D, 
                        const float* sin_tab, int tab_len, void* stream);
 
 /*
+ * Fused q_norm/k_norm + RoPE on a fused qkv row: q heads at columns [0, H*D)
+ * normalised with (qw, qb), k heads at [H*D, 2*H*D) with (kw, kb); one launch
+ * (vggt Attention.q_norm/k_norm + rope, ext; featureAligned_vggt.py:78).
+ * Same position/table conventions as vggt_headnorm_rope.
+ */
+int vggt_qknorm_rope(void* qkv, int64_t ld, int M, int H, int D, const float* qw, const float* qb, const float* kw,
+                     const float* kb, float eps, int rope_mode, const int32_t* pos, int period, const float* cos_tab,
+                     const float* sin_tab, int tab_len, void* stream);
+
+/*
  * Flash attention forward, bf16 in/out, fp32 online softmax, D in {64,128}.
  * For batch b, head h:  O = softmax(Q K^T * scale) V  with
  *   Q row i at q + (b*q_bstride + i)*ldq + h*D   (i < nq), same for K, V (j < nk)

@@ -35,6 +35,7 @@ _SIGS = {
     "vggt_dino_assemble": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp],
     "vggt_special_tokens": [_vp, _i64, _i, _i, _i, _i, _i, _vp, _vp],
     "vggt_copy_rows_f32": [_vp, _i64, _vp, _i64, _i, _i, _vp],
+    "vggt_qknorm_rope": [_vp, _i64, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _i, _vp, _i, _vp, _vp, _i, _vp],
     "vggt_layernorm_grouped": [_vp, _i, _i64, _vp, _vp, _f, _i, _i, _vp, _i, _i64, _i, _i, _i, _i, _i, _vp],
     "vggt_linear_f32": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _i, _vp, _i64, _vp, _vp],
     "vggt_attention_small": [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i64, _i, _i, _i, _i, _i, _i, _f,
@@ -136,6 +137,15 @@ def headnorm_rope(buf: torch.Tensor, col_off: int, H: int, D: int, w: Optional[t
     rc = lib().vggt_headnorm_rope(_p(buf), _ld(buf), col_off, M, H, D, _p(w), _p(b), float(eps), mode, _p(pos),
                                   period, _p(cos), _p(sin), tab, _stream())
     _check(rc, "vggt_headnorm_rope")
+
+
+def qknorm_rope(qkv: torch.Tensor, H: int, D: int, qw, qb, kw, kb, eps: float, mode: int = ROPE_NONE, pos=None,
+                period: int = 1, cos=None, sin=None) -> None:
+    _dev(qkv, "qknorm_rope")
+    tab = cos.shape[0] if cos is not None else 0
+    rc = lib().vggt_qknorm_rope(_p(qkv), _ld(qkv), qkv.shape[0], H, D, _p(qw), _p(qb), _p(kw), _p(kb), float(eps), mode,
+                                _p(pos), period, _p(cos), _p(sin), tab, _stream())
+    _check(rc, "vggt_qknorm_rope")
 
 
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, o: torch.Tensor, batch: int, heads: int, nq: int,

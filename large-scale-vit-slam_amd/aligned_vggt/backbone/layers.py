@@ -133,11 +133,10 @@ class Block(nn.Module):
         mode = rope.mode if (rope is not None and self.attn.rope is not None) else N.ROPE_NONE
         if qn is not None or mode != N.ROPE_NONE:
             rp = rope if mode != N.ROPE_NONE else None
-            for off, nm in ((0, qn), (C, kn)):
-                N.headnorm_rope(qkv, off, H, D, nm.weight if nm is not None else None,
-                                nm.bias if nm is not None else None, nm.eps if nm is not None else 0.0, mode,
-                                rp.pos if rp else None, rp.period if rp else 1, rp.cos if rp else None,
-                                rp.sin if rp else None)
+            N.qknorm_rope(qkv, H, D, qn.weight if qn is not None else None, qn.bias if qn is not None else None,
+                          kn.weight if kn is not None else None, kn.bias if kn is not None else None,
+                          qn.eps if qn is not None else 0.0, mode, rp.pos if rp else None, rp.period if rp else 1,
+                          rp.cos if rp else None, rp.sin if rp else None)
         ao = ws.buf("blk_ao", M, C, torch.bfloat16)
         nb, rows, n = groups
         N.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], ao, nb, H, n, n, D, rows, rows, rows, tag=tag)

@@ -4,7 +4,11 @@
 //
 // gfx950 design:
 //  * Workgroup = 4 waves = 128 query rows (32 per wave); KV tiles of 64 keys
-//    staged global->LDS by LDS-DMA (global_load_lds_dwordx4), double-buffered.
+//    staged global->LDS by LDS-DMA (buffer_load_dwordx4 ... lds),
+//    double-buffered.  The buffer descriptor is re-based per tile by SALU
+//    (base += 64 rows, num_records = remaining rows), so the per-lane offsets
+//    are loop-invariant (no VALU address math in the loop) and rows past nk
+//    read as zeros by the hardware range check.
 //  * "Swapped" QK^T: each wave computes S^T = K . Q^T with
 //    v_mfma_f32_32x32x16_bf16, so a lane owns one query row (lane & 31) and
 //    the two lanes l, l+32 hold all 64 keys of the tile -> the row max needs a
@@ -12,13 +16,18 @@
 //  * The S^T accumulator, rounded to bf16, is directly the B operand of
 //    O^T = V^T . P^T (no LDS round trip for P); the V^T A-operand comes from
 //    ds_read_b64_tr_b16 transposed reads of the row-major V tile.
-//  * LDS images are XOR-swizzled on the DMA source address so that the K
+//  * LDS images are XOR-swizzled on the DMA source offset so that the K
 //    ds_read_b128 fragment reads and the V transposed reads are bank-conflict
-//    free (chunk ^ ((key>>1)&7) / chunk ^ (((key>>1)&1)<<2) at D=64,
-//    chunk ^ (key&15) / chunk ^ ((key&3)<<2) at D=128).
+//    free; the swizzles touch only row bits that are lane-constant, so every
+//    LDS read is a loop-invariant base register + immediate offset (the tile
+//    loop is unrolled x2 so the double-buffer index is compile-time).
+//  * Online softmax in the log2 domain with a deferred rescale (T13): O and l
+//    are rescaled only when some row's max grows by more than THR=8 (P <= 2^8).
 //  * XCD-aware block order: consecutive query blocks of one (batch, head)
 //    share an XCD so its K/V stream is served from one L2.
 #include <math.h>
+
+#include <type_traits>
 
 #include "common.h"
 
@@ -26,21 +35,10 @@ namespace {
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(8))) short s16x8;
-
-// LDS-DMA of 16 B per lane into the wave-uniform LDS address `lds` (+lane*16).
-// Issued as inline asm so hipcc does not treat the pending LDS write as
-// aliasing the other buffer's reads (it otherwise drains vmcnt(0) before the
-// first transposed read of every tile); completion is waited for by the
-// explicit vmcnt(0) + barrier at the end of each tile.
-__device__ __forceinline__ void glds16(const void* g, uint32_t lds) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(g), "s"(lds)
-               : "memory");
-}
+typedef int int32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BQ = 128, BKV = 64, NT = 256;
+constexpr float THR = 8.0f;
 
 struct AttnArgs {
   const bf16_t* q;
@@ -52,6 +50,30 @@ struct AttnArgs {
   int batch, heads, nq, nk;
   float c;  // scale * log2(e)
 };
+
+// LDS-DMA: 16 B per lane from buffer `rsrc` at per-lane byte offset `voff`
+// into the wave-uniform LDS address `lds` (+lane*16).  Inline asm keeps the
+// pending LDS write invisible to hipcc's alias analysis (it would otherwise
+// drain vmcnt(0) before reads of the other buffer); completion is waited for
+// by the explicit vmcnt(0) + barrier at the end of every tile.
+__device__ __forceinline__ void dma16(int32x4 rsrc, uint32_t voff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rsrc), "s"(lds)
+               : "memory");
+}
+
+__device__ __forceinline__ int32x4 make_rsrc(const void* base, uint32_t nbytes) {
+  const uint64_t b = (uint64_t)base;
+  int32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  r[1] = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) & 0xffff;
+  r[2] = __builtin_amdgcn_readfirstlane(nbytes);
+  r[3] = 0x00020000;
+  return r;
+}
 
 template <int D>
 __device__ __forceinline__ int k_swz(int row, int chunk) {
@@ -66,18 +88,18 @@ __device__ __forceinline__ int v_swz(int row, int chunk) {
 
 template <int D>
 __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
-  constexpr int ROWB = D * 2;              // bytes per K/V row in LDS
-  constexpr int TILEB = BKV * ROWB;        // bytes per K (or V) tile
-  constexpr int RPI = 1024 / ROWB;         // rows per 1-KiB DMA instruction
-  constexpr int CPR = ROWB / 16;           // 16-B chunks per row
-  constexpr int IPW = TILEB / 1024 / 4;    // DMA instructions per wave per operand
-  constexpr int NKS = D / 16;              // k-steps of the QK^T MFMA
-  constexpr int NDB = D / 32;              // 32-row output blocks of O^T
+  constexpr int ROWB = D * 2;            // bytes per K/V row in LDS
+  constexpr int TILEB = BKV * ROWB;      // bytes per K (or V) tile
+  constexpr int NKS = D / 16;            // k-steps of the QK^T MFMA
+  constexpr int NDB = D / 32;            // 32-row output blocks of O^T
+  constexpr int RPI = 1024 / ROWB;       // rows per 1-KiB DMA instruction
+  constexpr int CPR = ROWB / 16;         // 16-B chunks per row
+  constexpr int IPW = TILEB / 1024 / 4;  // DMA instructions per wave per operand
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILEB];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int hl = lane >> 5;  // lane half
+  const int hl = lane >> 5;
   const int nqb = (a.nq + BQ - 1) / BQ;
   const int bid = xcd_remap(blockIdx.x, nqb * a.heads * a.batch);
   const int qb = bid % nqb;
@@ -89,58 +111,77 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
   const bf16_t* kp = a.k + (int64_t)b * a.kbs * a.ldk + h * D;
   const bf16_t* vp = a.v + (int64_t)b * a.vbs * a.ldv + h * D;
 
-  // Q fragments = B operand of S^T = K Q^T: Q[q][16ks + 8*hl + j]
+  // ---- Q fragments = B operand of S^T = K Q^T: Q[q][16ks + 8*hl + j]
   const int qrow = qb * BQ + wave * 32 + (lane & 31);
   const int qr = min(qrow, a.nq - 1);
   bf16x8 qf[NKS];
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) qf[ks] = *(const bf16x8*)(qp + (int64_t)qr * a.ldq + ks * 16 + 8 * hl);
-  // Retire the Q loads here: hipcc would otherwise place their vmcnt wait at
-  // the first use inside the tile loop, where it also drains the (uncounted)
-  // LDS-DMA prefetch of the next tile.
 #pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) asm volatile("" : "+v"(qf[ks]));
+  for (int ks = 0; ks < NKS; ++ks) asm volatile("" : "+v"(qf[ks]));  // retire the Q loads before the loop
 
-  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem));
-  auto stage = [&](int buf, int kv0) {
-    char* Ks = smem + buf * 2 * TILEB;
-    char* Vs = Ks + TILEB;
+  // ---- loop-invariant DMA offsets and LDS destinations
+  uint32_t koff[IPW], voff[IPW];
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) {
+    const int row = (wave * IPW + i) * RPI + lane / CPR;
+    const int cp = lane % CPR;
+    koff[i] = (uint32_t)(row * a.ldk + k_swz<D>(row, cp) * 8) * 2u;
+    voff[i] = (uint32_t)(row * a.ldv + v_swz<D>(row, cp) * 8) * 2u;
+  }
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem)) + wave * IPW * 1024;
+  const uint64_t kstep = (uint64_t)BKV * a.ldk * 2, vstep = (uint64_t)BKV * a.ldv * 2;
+  const uint64_t kbytes = (uint64_t)a.nk * a.ldk * 2, vbytes = (uint64_t)a.nk * a.ldv * 2;
+
+  auto stage = [&](int buf, int t) {
+    const uint64_t ko = kstep * t, vo = vstep * t;
+    const uint64_t kr_n = kbytes > ko ? kbytes - ko : 0, vr_n = vbytes > vo ? vbytes - vo : 0;
+    const int32x4 kr = make_rsrc((const char*)kp + ko, (uint32_t)(kr_n > 0xffffffffull ? 0xffffffffull : kr_n));
+    const int32x4 vr = make_rsrc((const char*)vp + vo, (uint32_t)(vr_n > 0xffffffffull ? 0xffffffffull : vr_n));
+    const uint32_t d = lds0 + buf * 2 * TILEB;
 #pragma unroll
     for (int i = 0; i < IPW; ++i) {
-      const int inst = wave * IPW + i;
-      const int row = inst * RPI + lane / CPR;
-      const int cp = lane % CPR;
-      const int src = min(kv0 + row, a.nk - 1);
-      glds16(kp + (int64_t)src * a.ldk + k_swz<D>(row, cp) * 8, lds_base + (uint32_t)(Ks - smem) + inst * 1024);
-      glds16(vp + (int64_t)src * a.ldv + v_swz<D>(row, cp) * 8, lds_base + (uint32_t)(Vs - smem) + inst * 1024);
+      dma16(kr, koff[i], d + i * 1024);
+      dma16(vr, voff[i], d + TILEB + i * 1024);
     }
   };
+
+  // ---- loop-invariant LDS read addresses (bytes within one K|V buffer pair)
+  uint32_t ka[NKS];
+  {
+    const int key = lane & 31;  // + kb*32: swizzle-invariant
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) ka[ks] = key * ROWB + (k_swz<D>(key, 2 * ks + hl) << 4);
+  }
+  uint32_t va[NDB];
+  {
+    const int g = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
+    const int r0 = 4 * hl + qq;  // + kb*32 + 16*ss + 8*half: swizzle-invariant
+#pragma unroll
+    for (int db = 0; db < NDB; ++db) {
+      const int col = db * 32 + 16 * g + 4 * pp;
+      va[db] = TILEB + r0 * ROWB + (v_swz<D>(r0, col >> 3) << 4) + (col & 7) * 2;
+    }
+  }
 
   f32x16 o[NDB];
 #pragma unroll
   for (int i = 0; i < NDB; ++i) o[i] = f32x16{};
   float m_run = -INFINITY, l_run = 0.f;
-
+  const float c = a.c;
   const int nt = (a.nk + BKV - 1) / BKV;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
 
-  for (int t = 0; t < nt; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nt) stage(cur ^ 1, (t + 1) * BKV);
-    const char* Ks = smem + cur * 2 * TILEB;
-    const char* Vs = Ks + TILEB;
-
-    // ---- S^T = K . Q^T for two 32-key blocks ----
+  auto tile = [&](auto bufc, int t) {
+    constexpr int BUF = decltype(bufc)::value;
+    const char* base = smem + BUF * 2 * TILEB;
+    // ---- S^T = K . Q^T for two 32-key blocks
     f32x16 s[2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
       s[kb] = f32x16{};
-      const int key = kb * 32 + (lane & 31);
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        const bf16x8 kf = *(const bf16x8*)(Ks + key * ROWB + (k_swz<D>(key, 2 * ks + hl) << 4));
+        const bf16x8 kf = *(const bf16x8*)(base + ka[ks] + kb * 32 * ROWB);
         s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kb], 0, 0, 0);
       }
     }
@@ -154,62 +195,70 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
           if (key >= a.nk) s[kb][r] = -INFINITY;
         }
     }
-    // ---- online softmax (log2 domain) ----
-    float mx = s[0][0];
+    // ---- row max (lane-partial over 32 keys, then the partner half)
+    float mx = fmaxf(s[0][0], s[0][1]);  // chained as v_max3_f32 (built with -fno-honor-nans)
 #pragma unroll
-    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s[0][r]);
+    for (int r = 2; r < 16; r += 2) mx = fmaxf(fmaxf(mx, s[0][r]), s[0][r + 1]);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[1][r]);
+    for (int r = 0; r < 16; r += 2) mx = fmaxf(fmaxf(mx, s[1][r]), s[1][r + 1]);
     {
       const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * c;
     }
-    const float m_new = fmaxf(m_run, mx * a.c);
-    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-    m_run = m_new;
+    // ---- deferred rescale: only when some row's max grew by > THR
+    if (__builtin_amdgcn_ballot_w64(mx > m_run + THR) != 0) {
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+      m_run = m_new;
+      l_run *= alpha;
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) o[db] *= alpha;
+    }
     float rs = 0.f;
     bf16x8 pf[2][2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
+      for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(s[kb][8 * ss + j], a.c, -m_new));
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[kb][8 * ss + j], c, -m_run));
           rs += p;
           pf[kb][ss][j] = (__bf16)p;
         }
-      }
-    l_run = l_run * alpha + rs;
+    l_run += rs;
+    // ---- O^T += V^T . P^T
 #pragma unroll
-    for (int db = 0; db < NDB; ++db) o[db] *= alpha;
-
-    // ---- O^T += V^T . P^T ----
-    const int g = (lane >> 4) & 1;
-    const int qq = (lane >> 2) & 3;
-    const int pp = lane & 3;
-#pragma unroll
-    for (int db = 0; db < NDB; ++db) {
-      const int col = db * 32 + 16 * g + 4 * pp;
+    for (int db = 0; db < NDB; ++db)
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
-          const int r0 = kb * 32 + 16 * ss + 4 * hl + qq;
-          const int r1 = r0 + 8;
-          const char* a0 = Vs + r0 * ROWB + (v_swz<D>(r0, col >> 3) << 4) + (col & 7) * 2;
-          const char* a1 = Vs + r1 * ROWB + (v_swz<D>(r1, col >> 3) << 4) + (col & 7) * 2;
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a0);
-          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a1);
+          const char* p0 = base + va[db] + (kb * 32 + 16 * ss) * ROWB;
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)LDS_PTR(p0));
+          const s16x4 hi =
+              __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)LDS_PTR(p0 + 8 * ROWB));
           const bf16x8 vf = __builtin_bit_cast(bf16x8, (s16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
           o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kb][ss], o[db], 0, 0, 0);
         }
-    }
+  };
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nt; t += 2) {
+    if (t + 1 < nt) stage(1, t + 1);
+    tile(std::integral_constant<int, 0>{}, t);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 >= nt) break;
+    if (t + 2 < nt) stage(0, t + 2);
+    tile(std::integral_constant<int, 1>{}, t + 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
-  // ---- epilogue: normalise, O[q][d] bf16 ----
+  // ---- epilogue: normalise, O[q][d] bf16
   {
     const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run), __float_as_uint(l_run), false, false);
     l_run = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
@@ -239,6 +288,8 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
   if (D != 64 && D != 128) return VGGT_ERR_UNSUPPORTED;
   if ((ldq | ldk | ldv | ldo) % 8 || ((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) % 16)
     return VGGT_ERR_ALIGN;
+  // per-lane 32-bit DMA offsets: one 64-row tile must span < 2 GiB
+  if ((uint64_t)BKV * (uint64_t)(ldk > ldv ? ldk : ldv) * 2 >= (1ull << 31)) return VGGT_ERR_SHAPE;
   AttnArgs a{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, ldq, ldk, ldv, ldo,
              q_bstride, k_bstride, v_bstride, o_bstride, batch, heads, nq, nk,
              scale * 1.4426950408889634f};

@@ -95,13 +95,16 @@ int launch_ln(const void* x, int in_bf, int64_t ldx, const float* w, const float
 // ------------------------------------------------- per-head norm + RoPE
 // One wave per row; each lane owns 8 consecutive values (one 16-B chunk) of
 // a head; LPH = D/8 lanes per head, heads processed 64/LPH at a time.
+// Heads [0, hsplit) use (w, b), heads [hsplit, H) use (w2, b2): one launch
+// normalises q and k of a fused qkv row (different q_norm / k_norm weights).
 template <int D, int MODE>
 __global__ __launch_bounds__(256) void headnorm_rope_kernel(bf16_t* __restrict__ buf, int64_t ld, int col_off, int M,
                                                             int H, const float* __restrict__ w,
                                                             const float* __restrict__ b, float eps,
                                                             const int32_t* __restrict__ pos, int period,
                                                             const float* __restrict__ cs, const float* __restrict__ sn,
-                                                            int tab_len) {
+                                                            int tab_len, int hsplit, const float* __restrict__ w2,
+                                                            const float* __restrict__ b2) {
   constexpr int LPH = D / 8;
   constexpr int HPP = 64 / LPH;  // heads per pass
   const int lane = threadIdx.x & 63;
@@ -118,16 +121,18 @@ __global__ __launch_bounds__(256) void headnorm_rope_kernel(bf16_t* __restrict__
     p0 = min(max(pos[row % period], 0), tab_len - 1);
   }
   float wv[8], bv[8];
-  if (w) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      wv[j] = w[e0 + j];
-      bv[j] = b ? b[e0 + j] : 0.f;
-    }
-  }
   for (int h0 = 0; h0 < H; h0 += HPP) {
     const int h = h0 + lane / LPH;
     const bool act = h < H;
+    if (w) {
+      const float* ww = h < hsplit ? w : w2;
+      const float* bb = h < hsplit ? b : b2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        wv[j] = ww[e0 + j];
+        bv[j] = bb ? bb[e0 + j] : 0.f;
+      }
+    }
     bf16_t* p = buf + (int64_t)row * ld + col_off + (act ? h : 0) * D + e0;
     float x[8];
     {
@@ -188,20 +193,21 @@ __global__ __launch_bounds__(256) void headnorm_rope_kernel(bf16_t* __restrict__
 
 template <int D>
 int launch_hnr(bf16_t* buf, int64_t ld, int col_off, int M, int H, const float* w, const float* b, float eps, int mode,
-               const int32_t* pos, int period, const float* cs, const float* sn, int tab_len, hipStream_t s) {
+               const int32_t* pos, int period, const float* cs, const float* sn, int tab_len, hipStream_t s,
+               int hsplit, const float* w2, const float* b2) {
   const int grid = (M + 3) / 4;
   switch (mode) {
     case VGGT_ROPE_NONE:
       headnorm_rope_kernel<D, VGGT_ROPE_NONE><<<grid, 256, 0, s>>>(buf, ld, col_off, M, H, w, b, eps, pos, period, cs,
-                                                                  sn, tab_len);
+                                                                  sn, tab_len, hsplit, w2, b2);
       break;
     case VGGT_ROPE_2D:
       headnorm_rope_kernel<D, VGGT_ROPE_2D><<<grid, 256, 0, s>>>(buf, ld, col_off, M, H, w, b, eps, pos, period, cs, sn,
-                                                                tab_len);
+                                                                tab_len, hsplit, w2, b2);
       break;
     case VGGT_ROPE_1D:
       headnorm_rope_kernel<D, VGGT_ROPE_1D><<<grid, 256, 0, s>>>(buf, ld, col_off, M, H, w, b, eps, pos, period, cs, sn,
-                                                                tab_len);
+                                                                tab_len, hsplit, w2, b2);
       break;
     default: return VGGT_ERR_UNSUPPORTED;
   }
@@ -254,6 +260,23 @@ extern "C" int vggt_headnorm_rope(void* buf, int64_t ld, int col_off, int M, int
     return VGGT_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
   if (D == 64) return launch_hnr<64>((bf16_t*)buf, ld, col_off, M, H, w, b, eps, rope_mode, pos, period, cos_tab, sin_tab,
-                                     tab_len, s);
-  return launch_hnr<128>((bf16_t*)buf, ld, col_off, M, H, w, b, eps, rope_mode, pos, period, cos_tab, sin_tab, tab_len, s);
+                                     tab_len, s, H, w, b);
+  return launch_hnr<128>((bf16_t*)buf, ld, col_off, M, H, w, b, eps, rope_mode, pos, period, cos_tab, sin_tab, tab_len, s,
+                         H, w, b);
+}
+
+extern "C" int vggt_qknorm_rope(void* qkv, int64_t ld, int M, int H, int D, const float* qw, const float* qb,
+                                const float* kw, const float* kb, float eps, int rope_mode, const int32_t* pos,
+                                int period, const float* cos_tab, const float* sin_tab, int tab_len, void* stream) {
+  if (M <= 0) return M == 0 ? VGGT_OK : VGGT_ERR_SHAPE;
+  if (H <= 0 || (D != 64 && D != 128)) return VGGT_ERR_SHAPE;
+  if ((ld % 8) || ((uintptr_t)qkv % 16)) return VGGT_ERR_ALIGN;
+  if ((qw == nullptr) != (kw == nullptr)) return VGGT_ERR_SHAPE;
+  if (rope_mode != VGGT_ROPE_NONE && (!pos || !cos_tab || !sin_tab || period <= 0 || tab_len <= 0))
+    return VGGT_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  if (D == 64) return launch_hnr<64>((bf16_t*)qkv, ld, 0, M, 2 * H, qw, qb, eps, rope_mode, pos, period, cos_tab,
+                                     sin_tab, tab_len, s, H, kw, kb);
+  return launch_hnr<128>((bf16_t*)qkv, ld, 0, M, 2 * H, qw, qb, eps, rope_mode, pos, period, cos_tab, sin_tab, tab_len,
+                         s, H, kw, kb);
 }
