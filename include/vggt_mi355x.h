@@ -47,14 +47,22 @@ extern "C" {
 /* Library identification (build string) -- for load checks. */
 const char* vggt_version(void);
 
+/* Process-wide kernel-variant knobs (defaults: the VGGT_GEMM / VGGT_ATTN_WAVES
+ * environment variables, else the tuned choice).  Returns the previous value,
+ * or VGGT_ERR_UNSUPPORTED for an unknown knob / value.  Results do not depend
+ * on the variant beyond fp32 summation order inside one MFMA tile. */
+#define VGGT_TUNE_GEMM_TILE 1  /* -1 auto, 0: 128x128 tile, 1: 256x256 ring, 2: 256x128 ring */
+#define VGGT_TUNE_ATTN_WAVES 2 /* 4 or 8 waves (128 / 256 query rows) per attention workgroup */
+int vggt_tune(int knob, int value);
+
 /*
  * out[M,N] = epi( A[M,K] . W[N,K]^T + bias[N] ), bf16 MFMA (v_mfma_f32_16x16x32_bf16),
  * fp32 accumulation.  Replaces every autocast nn.Linear on the bf16 tier:
  * vggt Attention.qkv/proj, Mlp.fc1/fc2 (aggregator / DINOv2 blocks, via
  * featureAligned_vggt.py:78), CrossAttention.q/k/v/proj (cross_attention.py:37-43,55-57,76),
  * AlignmentHead.project_in (alignment_head.py:242), and the DINOv2 patch-embed
- * conv as an im2col GEMM.  Requires N % 128 == 0, K % 64 == 0, 16-B aligned
- * rows; A must have >= roundup(M,128) readable rows.  `gamma`/`out2`/`ldo2`
+ * conv as an im2col GEMM.  Requires N % 128 == 0, K % 32 == 0, 16-B aligned
+ * rows (rows past M are never read or written).  `gamma`/`out2`/`ldo2`
  * are used by VGGT_EPI_RESID_F32 only (LayerScale; out2 may be NULL).
  */
 int vggt_gemm_bf16(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int M, int N, int K,

@@ -26,6 +26,7 @@ _ERR = {VGGT_ERR_SHAPE: "unsupported or inconsistent shape", VGGT_ERR_ALIGN: "mi
 
 _vp, _i, _i64, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
 _SIGS = {
+    "vggt_tune": [_i, _i],
     "vggt_gemm_bf16": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _vp, _i64, _vp, _vp, _i64, _vp],
     "vggt_layernorm": [_vp, _i, _i64, _vp, _vp, _f, _i, _i, _vp, _i, _i64, _vp],
     "vggt_headnorm_rope": [_vp, _i64, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _i, _vp, _vp, _i, _vp],
@@ -75,6 +76,18 @@ def lib() -> ctypes.CDLL:
 
 def version() -> str:
     return lib().vggt_version().decode()
+
+
+TUNE_GEMM_TILE = 1
+TUNE_ATTN_WAVES = 2
+
+
+def tune(knob: int, value: int) -> int:
+    """vggt_tune: set a process-wide kernel-variant knob, return the previous value."""
+    rc = lib().vggt_tune(knob, value)
+    if rc == VGGT_ERR_UNSUPPORTED:
+        raise ValueError(f"vggt_tune: unsupported knob/value ({knob}, {value})")
+    return rc
 
 
 def _check(rc: int, name: str) -> None:

@@ -26,10 +26,12 @@
 //  * XCD-aware block order: consecutive query blocks of one (batch, head)
 //    share an XCD so its K/V stream is served from one L2.
 #include <math.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
 #include "common.h"
+#include "tune.h"
 
 namespace {
 
@@ -37,7 +39,7 @@ typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(8))) short s16x8;
 typedef int int32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BQ = 128, BKV = 64, NT = 256;
+constexpr int BKV = 64;
 constexpr float THR = 8.0f;
 
 struct AttnArgs {
@@ -86,20 +88,27 @@ __device__ __forceinline__ int v_swz(int row, int chunk) {
   else return chunk ^ ((row & 3) << 2);
 }
 
-template <int D>
-__global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
+template <int D, int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
+  constexpr int BQ = NW * 32;            // query rows per workgroup (32 per wave)
   constexpr int ROWB = D * 2;            // bytes per K/V row in LDS
   constexpr int TILEB = BKV * ROWB;      // bytes per K (or V) tile
   constexpr int NKS = D / 16;            // k-steps of the QK^T MFMA
   constexpr int NDB = D / 32;            // 32-row output blocks of O^T
   constexpr int RPI = 1024 / ROWB;       // rows per 1-KiB DMA instruction
   constexpr int CPR = ROWB / 16;         // 16-B chunks per row
-  constexpr int IPW = TILEB / 1024 / 4;  // DMA instructions per wave per operand
+  constexpr int IPW = TILEB / 1024 / NW;  // DMA instructions per wave per operand
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILEB];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int hl = lane >> 5;
+  // 8-wave form: the second-dispatched half (waves 4-7) shares each SIMD with
+  // an older wave and loses VALU arbitration on every segment; one static
+  // priority raise for it (cdna_hip_programming.md T5, static form).
+  if constexpr (NW == 8) {
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  }
   const int nqb = (a.nq + BQ - 1) / BQ;
   const int bid = xcd_remap(blockIdx.x, nqb * a.heads * a.batch);
   const int qb = bid % nqb;
@@ -293,10 +302,19 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
   AttnArgs a{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, ldq, ldk, ldv, ldo,
              q_bstride, k_bstride, v_bstride, o_bstride, batch, heads, nq, nk,
              scale * 1.4426950408889634f};
-  const int nwg = ((nq + BQ - 1) / BQ) * heads * batch;
+  // 8-wave workgroups (256 query rows) for long sequences; 4-wave ones
+  // (128 rows) when the query count is short enough that the padding of a
+  // 256-row block would cost more than the pairing gains.
+  const int nw = (g_vggt_attn_waves == 8 && nq >= 4096) ? 8 : 4;
+  const int nwg = ((nq + nw * 32 - 1) / (nw * 32)) * heads * batch;
   hipStream_t s = (hipStream_t)stream;
-  if (D == 64) attn_fwd_kernel<64><<<nwg, NT, 0, s>>>(a);
-  else attn_fwd_kernel<128><<<nwg, NT, 0, s>>>(a);
+  if (nw == 8) {
+    if (D == 64) attn_fwd_kernel<64, 8><<<nwg, 512, 0, s>>>(a);
+    else attn_fwd_kernel<128, 8><<<nwg, 512, 0, s>>>(a);
+  } else {
+    if (D == 64) attn_fwd_kernel<64, 4><<<nwg, 256, 0, s>>>(a);
+    else attn_fwd_kernel<128, 4><<<nwg, 256, 0, s>>>(a);
+  }
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
 }

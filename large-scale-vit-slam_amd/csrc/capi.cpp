@@ -2,3 +2,34 @@
 #include "../../include/vggt_mi355x.h"
 
 extern "C" const char* vggt_version(void) { return "vggt_mi355x 0.1 gfx950"; }
+
+#include <stdlib.h>
+
+#include "tune.h"
+
+namespace {
+int env_or(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+}  // namespace
+
+int g_vggt_gemm_tile = env_or("VGGT_GEMM", -1);
+int g_vggt_attn_waves = env_or("VGGT_ATTN_WAVES", 4);
+
+extern "C" int vggt_tune(int knob, int value) {
+  int prev;
+  switch (knob) {
+    case VGGT_TUNE_GEMM_TILE:
+      if (value < -1 || value > 2) return VGGT_ERR_UNSUPPORTED;
+      prev = g_vggt_gemm_tile;
+      g_vggt_gemm_tile = value;
+      return prev;
+    case VGGT_TUNE_ATTN_WAVES:
+      if (value != 4 && value != 8) return VGGT_ERR_UNSUPPORTED;
+      prev = g_vggt_attn_waves;
+      g_vggt_attn_waves = value;
+      return prev;
+    default: return VGGT_ERR_UNSUPPORTED;
+  }
+}

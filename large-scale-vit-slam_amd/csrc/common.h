@@ -28,6 +28,28 @@ __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f)); }
 
+// GELU(x) = x * Phi(x) through a branch-free erfc (Chebyshev fit, fractional
+// error < 1.2e-7 over the whole real line, i.e. ~1 fp32 ulp): one rcp, one
+// exp2 and ten FMAs, no divergence.  Used where the result is rounded to
+// bf16 (the GEMM fc1 epilogue), where it matches the libm erf form up to
+// rare round-to-nearest ties.
+__device__ __forceinline__ float gelu_fast(float x) {
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
+  float p = 0.17087277f;
+  p = fmaf(p, t, -0.82215223f);
+  p = fmaf(p, t, 1.48851587f);
+  p = fmaf(p, t, -1.13520398f);
+  p = fmaf(p, t, 0.27886807f);
+  p = fmaf(p, t, -0.18628806f);
+  p = fmaf(p, t, 0.09678418f);
+  p = fmaf(p, t, 0.37409196f);
+  p = fmaf(p, t, 1.00002368f);
+  p = fmaf(p, t, -1.26551223f);
+  const float e = t * __builtin_amdgcn_exp2f(fmaf(-z, z, p) * 1.4426950408889634f);  // erfc(z)
+  return x * (x >= 0.f ? fmaf(-0.5f, e, 1.0f) : 0.5f * e);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

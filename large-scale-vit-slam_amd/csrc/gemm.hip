@@ -16,7 +16,10 @@
 //    and written with 16-B coalesced stores (fp32 residual read-modify-write
 //    likewise), applying bias / GELU / LayerScale+residual there.
 //  * XCD-aware bijective block remap so the N-tiles of one M-panel share an L2.
+#include <stdlib.h>
+
 #include "common.h"
+#include "tune.h"
 
 namespace {
 
@@ -33,6 +36,72 @@ struct Epi {
   float* out2;
   int64_t ldo2;
 };
+
+// ---- epilogue 2 (shared): the bf16 C tile staged in LDS (row stride CROW
+// bytes) re-read as whole rows, 16 B (8 features) per thread, and written with
+// coalesced stores, applying GELU / LayerScale + fp32 residual there.
+template <int EPI, int BM, int BN, int NT, int CROW>
+__device__ __forceinline__ void write_tile(const char* Cs, int m0, int n0, int M, const Epi& ep) {
+  constexpr int CPR = BN / 8;        // 16-B chunks per row
+  constexpr int RPP = NT / CPR;      // rows per pass
+  const int ch = threadIdx.x % CPR;
+  const int n = n0 + ch * 8;
+  float g[8];
+  if constexpr (EPI == VGGT_EPI_RESID_F32) {
+    const f32x4 g0 = *(const f32x4*)(ep.gamma + n);
+    const f32x4 g1 = *(const f32x4*)(ep.gamma + n + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      g[j] = g0[j];
+      g[4 + j] = g1[j];
+    }
+  }
+#pragma unroll 2
+  for (int it = 0; it < BM / RPP; ++it) {
+    const int ml = it * RPP + threadIdx.x / CPR;
+    const int m = m0 + ml;
+    if (m >= M) continue;
+    const uint4 cv = *(const uint4*)(Cs + ml * CROW + ch * 16);
+    if constexpr (EPI == VGGT_EPI_BF16) {
+      *(uint4*)((bf16_t*)ep.out + (int64_t)m * ep.ldo + n) = cv;
+    } else {
+      const uint32_t w4[4] = {cv.x, cv.y, cv.z, cv.w};
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[2 * j] = bf2f((bf16_t)(w4[j] & 0xffff));
+        v[2 * j + 1] = bf2f((bf16_t)(w4[j] >> 16));
+      }
+      if constexpr (EPI == VGGT_EPI_GELU_BF16) {
+        uint4 o;
+        o.x = pack_bf2(gelu_fast(v[0]), gelu_fast(v[1]));
+        o.y = pack_bf2(gelu_fast(v[2]), gelu_fast(v[3]));
+        o.z = pack_bf2(gelu_fast(v[4]), gelu_fast(v[5]));
+        o.w = pack_bf2(gelu_fast(v[6]), gelu_fast(v[7]));
+        *(uint4*)((bf16_t*)ep.out + (int64_t)m * ep.ldo + n) = o;
+      } else if constexpr (EPI == VGGT_EPI_RESID_F32) {
+        float* xp = (float*)ep.out + (int64_t)m * ep.ldo + n;
+        f32x4 x0 = *(f32x4*)xp, x1 = *(f32x4*)(xp + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          x0[j] += g[j] * v[j];
+          x1[j] += g[4 + j] * v[4 + j];
+        }
+        *(f32x4*)xp = x0;
+        *(f32x4*)(xp + 4) = x1;
+        if (ep.out2) {
+          float* yp = ep.out2 + (int64_t)m * ep.ldo2 + n;
+          *(f32x4*)yp = x0;
+          *(f32x4*)(yp + 4) = x1;
+        }
+      } else {  // VGGT_EPI_F32
+        float* yp = (float*)ep.out + (int64_t)m * ep.ldo + n;
+        *(f32x4*)yp = f32x4{v[0], v[1], v[2], v[3]};
+        *(f32x4*)(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      }
+    }
+  }
+}
 
 template <int EPI>
 __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(const bf16_t* __restrict__ A, int64_t lda,
@@ -119,64 +188,210 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(const bf16_t* __restri
   }
   __syncthreads();
 
-  // ---- epilogue 2: coalesced row write-out ----
-  const int ch = threadIdx.x & 15;  // 16-B chunk (8 features) within the 128-wide row
-  const int n = n0 + ch * 8;
-  float g[8];
-  if constexpr (EPI == VGGT_EPI_RESID_F32) {
-    const f32x4 g0 = *(const f32x4*)(ep.gamma + n);
-    const f32x4 g1 = *(const f32x4*)(ep.gamma + n + 4);
+  write_tile<EPI, BM, BN, NT, CROW>(Cs, m0, n0, M, ep);
+}
+
+
+// ===========================================================================
+// Large-tile form: 256 x BN (BN = 256 or 128) block tile, 8 waves, BK = 32,
+// a 4-slot LDS ring filled by buffer_load ... lds (LDS-DMA) three K-steps
+// ahead, ONE barrier per K-step behind a COUNTED vmcnt, so the prefetch stays
+// in flight across barriers (cdna_hip_programming.md §5 "what does break the
+// ~900 TF ceiling").  64-B LDS rows; the swizzle chunk ^ h((row >> 2) & 3),
+// h = {0,3,2,1}, makes every ds_read_b128 fragment read conflict-free over the
+// four 16-lane groups; it is applied on the DMA source offset (the DMA image
+// is lane-linear) and on the read.
+// ===========================================================================
+typedef int int32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int RBM = 256, RBK = 32, RNT = 512, RSLOTS = 4;
+
+__device__ __forceinline__ int32x4 make_rsrc_u(const void* base) {
+  const uint64_t b = (uint64_t)base;
+  int32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  r[1] = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) & 0xffff;
+  r[2] = -1;  // num_records: whole 4 GiB window (offsets are bounded by the caller)
+  r[3] = 0x00020000;
+  return r;
+}
+
+// 16 B per lane from (rsrc, voff + soff) into LDS at the wave-uniform address
+// `lds` (+ lane * 16).  Kept in asm so hipcc's alias analysis does not drain
+// vmcnt before the ring's ds_reads; completion is tracked by the counted
+// vmcnt + barrier in the K-loop.
+__device__ __forceinline__ void dma16s(int32x4 rsrc, uint32_t voff, uint32_t soff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds)
+               : "memory");
+}
+
+__device__ __forceinline__ int ring_swz(int row, int chunk) { return chunk ^ ((4 - ((row >> 2) & 3)) & 3); }
+
+template <int BN>
+struct RingCfg {
+  static constexpr int WM = BN == 256 ? 2 : 4;     // waves along M
+  static constexpr int WN = 8 / WM;                // waves along N
+  static constexpr int TM = RBM / WM;              // wave tile rows (M)
+  static constexpr int TN = BN / WN;               // wave tile cols (N)
+  static constexpr int MI = TM / 16, NI = TN / 16; // 16x16 fragments
+  static constexpr int ABYTES = RBM * RBK * 2;     // 16 KiB
+  static constexpr int WBYTES = BN * RBK * 2;
+  static constexpr int SLOT = ABYTES + WBYTES;
+  static constexpr int AL = ABYTES / 1024 / 8;     // DMA instructions per wave per stage (A)
+  static constexpr int WL = WBYTES / 1024 / 8;     // (W)
+  static constexpr int LPS = AL + WL;              // vmcnt units per stage
+  static constexpr int CROW = BN * 2 + 16;
+  static constexpr int LDS = (RSLOTS * SLOT > RBM * CROW) ? RSLOTS * SLOT : RBM * CROW;
+};
+
+template <int EPI, int BN>
+__global__ __launch_bounds__(RNT, 1) void gemm_ring_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                           const bf16_t* __restrict__ W, int64_t ldw, int M, int N,
+                                                           int K, Epi ep) {
+  using C = RingCfg<BN>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tiles_n = N / BN;
+  const int tiles_m = (M + RBM - 1) / RBM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (t / tiles_n) * RBM;
+  const int n0 = (t % tiles_n) * BN;
+  const int nk = K / RBK;
+
+  // ---- loop-invariant DMA offsets: instruction i of this wave covers rows
+  // (wave*L + i)*16 + lane/4, source chunk swizzled; rows past M clamp to M-1.
+  const int32x4 ra = make_rsrc_u(A + (int64_t)m0 * lda);
+  const int32x4 rw = make_rsrc_u(W + (int64_t)n0 * ldw);
+  uint32_t aoff[C::AL], woff[C::WL];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      g[j] = g0[j];
-      g[4 + j] = g1[j];
-    }
+  for (int i = 0; i < C::AL; ++i) {
+    const int row = (wave * C::AL + i) * 16 + (lane >> 2);
+    const int rr = min(m0 + row, M - 1) - m0;
+    aoff[i] = (uint32_t)(rr * lda + ring_swz(row, lane & 3) * 8) * 2u;
   }
-#pragma unroll 2
-  for (int it = 0; it < BM / 16; ++it) {
-    const int ml = it * 16 + (threadIdx.x >> 4);
-    const int m = m0 + ml;
-    if (m >= M) continue;
-    const uint4 cv = *(const uint4*)(Cs + ml * CROW + ch * 16);
-    if constexpr (EPI == VGGT_EPI_BF16) {
-      *(uint4*)((bf16_t*)ep.out + (int64_t)m * ep.ldo + n) = cv;
+#pragma unroll
+  for (int i = 0; i < C::WL; ++i) {
+    const int row = (wave * C::WL + i) * 16 + (lane >> 2);
+    woff[i] = (uint32_t)(row * ldw + ring_swz(row, lane & 3) * 8) * 2u;
+  }
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem));
+  auto stage = [&](int kt) {
+    const uint32_t slot = lds0 + (kt & (RSLOTS - 1)) * C::SLOT;
+    const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(kt * RBK * 2));
+#pragma unroll
+    for (int i = 0; i < C::AL; ++i) dma16s(ra, aoff[i], soff, slot + (wave * C::AL + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < C::WL; ++i) dma16s(rw, woff[i], soff, slot + C::ABYTES + (wave * C::WL + i) * 1024);
+  };
+
+  // ---- loop-invariant fragment read offsets (row & 15 == lane & 15)
+  const int wm = wave / C::WN, wn = wave % C::WN;
+  const int fr = lane & 15, fc = lane >> 4;
+  const uint32_t lane_off = fr * 64 + (ring_swz(fr, fc) << 4);
+  const uint32_t a_off = (wm * C::TM) * 64 + lane_off;
+  const uint32_t w_off = C::ABYTES + (wn * C::TN) * 64 + lane_off;
+
+  f32x4 acc[C::NI][C::MI];
+#pragma unroll
+  for (int i = 0; i < C::NI; ++i)
+#pragma unroll
+    for (int j = 0; j < C::MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- K-loop.  Step j's fragments are read into registers during step
+  // j-1's MFMAs (register double buffer F0/F1), so a slot is free for
+  // restaging as soon as its reads retired: the DMA runs four steps ahead.
+  auto wait_landed = [&](int newer) {  // own DMA with `newer` later stages still in flight, then everyone's
+    if constexpr (C::LPS == 4) {
+      if (newer >= 3) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+      else if (newer == 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+      else if (newer == 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     } else {
-      const uint32_t w4[4] = {cv.x, cv.y, cv.z, cv.w};
-      float v[8];
+      if (newer >= 3) asm volatile("s_waitcnt vmcnt(9)\n\ts_barrier" ::: "memory");
+      else if (newer == 2) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+      else if (newer == 1) asm volatile("s_waitcnt vmcnt(3)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  };
+  auto read_frags = [&](int kt, bf16x8(&wf)[C::NI], bf16x8(&af)[C::MI]) {
+    const char* base = smem + (kt & (RSLOTS - 1)) * C::SLOT;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[2 * j] = bf2f((bf16_t)(w4[j] & 0xffff));
-        v[2 * j + 1] = bf2f((bf16_t)(w4[j] >> 16));
-      }
-      if constexpr (EPI == VGGT_EPI_GELU_BF16) {
-        uint4 o;
-        o.x = pack_bf2(gelu_erf(v[0]), gelu_erf(v[1]));
-        o.y = pack_bf2(gelu_erf(v[2]), gelu_erf(v[3]));
-        o.z = pack_bf2(gelu_erf(v[4]), gelu_erf(v[5]));
-        o.w = pack_bf2(gelu_erf(v[6]), gelu_erf(v[7]));
-        *(uint4*)((bf16_t*)ep.out + (int64_t)m * ep.ldo + n) = o;
-      } else if constexpr (EPI == VGGT_EPI_RESID_F32) {
-        float* xp = (float*)ep.out + (int64_t)m * ep.ldo + n;
-        f32x4 x0 = *(f32x4*)xp, x1 = *(f32x4*)(xp + 4);
+    for (int i = 0; i < C::NI; ++i) wf[i] = *(const bf16x8*)(base + w_off + i * 16 * 64);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          x0[j] += g[j] * v[j];
-          x1[j] += g[4 + j] * v[4 + j];
-        }
-        *(f32x4*)xp = x0;
-        *(f32x4*)(xp + 4) = x1;
-        if (ep.out2) {
-          float* yp = ep.out2 + (int64_t)m * ep.ldo2 + n;
-          *(f32x4*)yp = x0;
-          *(f32x4*)(yp + 4) = x1;
-        }
-      } else {  // VGGT_EPI_F32
-        float* yp = (float*)ep.out + (int64_t)m * ep.ldo + n;
-        *(f32x4*)yp = f32x4{v[0], v[1], v[2], v[3]};
-        *(f32x4*)(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
-      }
+    for (int i = 0; i < C::MI; ++i) af[i] = *(const bf16x8*)(base + a_off + i * 16 * 64);
+  };
+  // one K-step: MFMAs on (cw, ca) with the next step's reads into (nw, na)
+  // issued after the first MI of them (sched_group_barrier pins the order)
+  auto step = [&](int kt, bf16x8(&cw)[C::NI], bf16x8(&ca)[C::MI], bf16x8(&nw)[C::NI], bf16x8(&na)[C::MI]) {
+    // this step's fragments retired (and with them every read of slot kt, which
+    // is restaged below); step kt+1 landed for every wave
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (kt + 1 < nk) wait_landed(min(nk - 2 - kt, 2));
+    else asm volatile("s_barrier" ::: "memory");
+    if (kt + 4 < nk) stage(kt + 4);
+    read_frags(kt + 1, nw, na);  // unconditional (a stale slot on the last step, unused): keeps one basic block
+#pragma unroll
+    for (int mi = 0; mi < C::MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < C::NI; ++ni)
+        acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cw[ni], ca[mi], acc[ni][mi], 0, 0, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, C::NI, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, C::NI + C::MI, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, C::NI * (C::MI - 1), 0);
+  };
+
+  stage(0);
+  if (nk > 1) stage(1);
+  if (nk > 2) stage(2);
+  if (nk > 3) stage(3);
+  wait_landed(min(nk - 1, 3));
+  bf16x8 w0[C::NI], a0[C::MI], w1[C::NI], a1[C::MI];
+  read_frags(0, w0, a0);
+  for (int kt = 0; kt < nk; kt += 2) {
+    step(kt, w0, a0, w1, a1);
+    if (kt + 1 < nk) step(kt + 1, w1, a1, w0, a0);
+  }
+  // all waves done with the ring (no DMA or read pending): reuse it as the C tile
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  // ---- epilogue 1: acc (C^T fragments) + bias -> bf16 C tile in LDS ----
+  char* Cs = smem;
+#pragma unroll
+  for (int ni = 0; ni < C::NI; ++ni) {
+    const int nl = wn * C::TN + ni * 16 + 4 * (lane >> 4);
+    const f32x4 bv = *(const f32x4*)(ep.bias + n0 + nl);
+#pragma unroll
+    for (int mi = 0; mi < C::MI; ++mi) {
+      const int ml = wm * C::TM + mi * 16 + (lane & 15);
+      uint2 pk;
+      pk.x = pack_bf2(acc[ni][mi][0] + bv[0], acc[ni][mi][1] + bv[1]);
+      pk.y = pack_bf2(acc[ni][mi][2] + bv[2], acc[ni][mi][3] + bv[3]);
+      *(uint2*)(Cs + ml * C::CROW + nl * 2) = pk;
     }
   }
+  __syncthreads();
+  write_tile<EPI, RBM, BN, RNT, C::CROW>(Cs, m0, n0, M, ep);
+}
+
+template <int EPI, int BN>
+int launch_ring(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int M, int N, int K, const Epi& ep,
+                hipStream_t s) {
+  using C = RingCfg<BN>;
+  static bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)gemm_ring_kernel<EPI, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              C::LDS);
+    return true;
+  }();
+  (void)attr;
+  const int nwg = ((M + RBM - 1) / RBM) * (N / BN);
+  gemm_ring_kernel<EPI, BN><<<nwg, RNT, C::LDS, s>>>(a, lda, w, ldw, M, N, K, ep);
+  return VGGT_OK;
 }
 
 }  // namespace
@@ -184,17 +399,50 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(const bf16_t* __restri
 extern "C" int vggt_gemm_bf16(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int M, int N,
                               int K, int epi, void* out, int64_t ldo, const float* gamma, float* out2, int64_t ldo2,
                               void* stream) {
-  if (M <= 0 || N <= 0 || K <= 0 || N % BN || K % BK) return VGGT_ERR_SHAPE;
+  if (M <= 0 || N <= 0 || K <= 0 || N % 128 || K % 32) return VGGT_ERR_SHAPE;
   if ((lda % 8) || (ldw % 8) || ((uintptr_t)A & 15) || ((uintptr_t)W & 15) || ((uintptr_t)bias & 15))
     return VGGT_ERR_ALIGN;
   if (epi == VGGT_EPI_RESID_F32 && (!gamma || ((uintptr_t)gamma & 15) || (out2 && (ldo2 % 4))))
     return VGGT_ERR_ALIGN;
   if ((epi == VGGT_EPI_BF16 || epi == VGGT_EPI_GELU_BF16) ? (ldo % 8) : (ldo % 4)) return VGGT_ERR_ALIGN;
   Epi ep{bias, out, ldo, gamma, out2, ldo2};
-  const int nwg = ((M + BM - 1) / BM) * (N / BN);
   hipStream_t s = (hipStream_t)stream;
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* w = (const bf16_t*)W;
+  // Tile choice (vggt_tune VGGT_TUNE_GEMM_TILE): 0 the 128x128 form, 1 the
+  // 256x256 ring, 2 the 256x128 ring.  Auto (-1): the 256x256 ring for the wide
+  // projections (N >= 2048: qkv, fc1 -- measured 7-14% faster on the aggregator
+  // shapes), the 128x128 form for N = 1024 (proj, fc2), where 256x256 tiles
+  // leave the last of only ~1.3 rounds of workgroups mostly idle.
+  int mode = g_vggt_gemm_tile;
+  if (mode < 0) mode = (N >= 2048 && N % 256 == 0 && M >= 1024) ? 1 : 0;
+  if (mode == 0 && K % BK) mode = 2;     // the 128x128 form steps K by 64
+  if (mode == 1 && N % 256) mode = 2;
+  // per-lane 32-bit DMA offsets span one 256-row panel
+  if (mode != 0 && (int64_t)RBM * (lda > ldw ? lda : ldw) * 2 >= (1ll << 31)) return VGGT_ERR_SHAPE;
+  if (mode == 1) {
+    switch (epi) {
+      case VGGT_EPI_BF16: launch_ring<VGGT_EPI_BF16, 256>(a, lda, w, ldw, M, N, K, ep, s); break;
+      case VGGT_EPI_GELU_BF16: launch_ring<VGGT_EPI_GELU_BF16, 256>(a, lda, w, ldw, M, N, K, ep, s); break;
+      case VGGT_EPI_RESID_F32: launch_ring<VGGT_EPI_RESID_F32, 256>(a, lda, w, ldw, M, N, K, ep, s); break;
+      case VGGT_EPI_F32: launch_ring<VGGT_EPI_F32, 256>(a, lda, w, ldw, M, N, K, ep, s); break;
+      default: return VGGT_ERR_UNSUPPORTED;
+    }
+    HIP_LAUNCH_CHECK();
+    return VGGT_OK;
+  }
+  if (mode == 2) {
+    switch (epi) {
+      case VGGT_EPI_BF16: launch_ring<VGGT_EPI_BF16, 128>(a, lda, w, ldw, M, N, K, ep, s); break;
+      case VGGT_EPI_GELU_BF16: launch_ring<VGGT_EPI_GELU_BF16, 128>(a, lda, w, ldw, M, N, K, ep, s); break;
+      case VGGT_EPI_RESID_F32: launch_ring<VGGT_EPI_RESID_F32, 128>(a, lda, w, ldw, M, N, K, ep, s); break;
+      case VGGT_EPI_F32: launch_ring<VGGT_EPI_F32, 128>(a, lda, w, ldw, M, N, K, ep, s); break;
+      default: return VGGT_ERR_UNSUPPORTED;
+    }
+    HIP_LAUNCH_CHECK();
+    return VGGT_OK;
+  }
+  const int nwg = ((M + BM - 1) / BM) * (N / BN);
   switch (epi) {
     case VGGT_EPI_BF16: gemm_bf16_kernel<VGGT_EPI_BF16><<<nwg, NT, 0, s>>>(a, lda, w, ldw, M, N, K, ep); break;
     case VGGT_EPI_GELU_BF16: gemm_bf16_kernel<VGGT_EPI_GELU_BF16><<<nwg, NT, 0, s>>>(a, lda, w, ldw, M, N, K, ep); break;

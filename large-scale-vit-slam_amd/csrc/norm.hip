@@ -120,18 +120,26 @@ __global__ __launch_bounds__(256) void headnorm_rope_kernel(bf16_t* __restrict__
   } else if constexpr (MODE == VGGT_ROPE_1D) {
     p0 = min(max(pos[row % period], 0), tab_len - 1);
   }
-  float wv[8], bv[8];
+  // both weight sets preloaded (heads < hsplit use w/b, the rest w2/b2)
+  float wa[8], ba[8], wb[8], bb2[8];
+  if (w) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      wa[j] = w[e0 + j];
+      ba[j] = b ? b[e0 + j] : 0.f;
+      wb[j] = w2[e0 + j];
+      bb2[j] = b2 ? b2[e0 + j] : 0.f;
+    }
+  }
   for (int h0 = 0; h0 < H; h0 += HPP) {
     const int h = h0 + lane / LPH;
     const bool act = h < H;
-    if (w) {
-      const float* ww = h < hsplit ? w : w2;
-      const float* bb = h < hsplit ? b : b2;
+    const bool first_set = h < hsplit;
+    float wv[8], bv[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        wv[j] = ww[e0 + j];
-        bv[j] = bb ? bb[e0 + j] : 0.f;
-      }
+    for (int j = 0; j < 8; ++j) {
+      wv[j] = first_set ? wa[j] : wb[j];
+      bv[j] = first_set ? ba[j] : bb2[j];
     }
     bf16_t* p = buf + (int64_t)row * ld + col_off + (act ? h : 0) * D + e0;
     float x[8];

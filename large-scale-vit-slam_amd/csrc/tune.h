@@ -1,0 +1,4 @@
+// Process-wide kernel-variant knobs behind vggt_tune() (capi.cpp).
+#pragma once
+extern int g_vggt_gemm_tile;   // -1 auto, 0 128x128, 1 256x256 ring, 2 256x128 ring
+extern int g_vggt_attn_waves;  // 4 or 8

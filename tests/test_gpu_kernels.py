@@ -62,9 +62,39 @@ def test_gemm_epilogues(N, M, Nn, K, epi):
         assert _rel(out, refb) < 4e-3
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("M,Nn,K", [(300, 256, 96), (1000, 768, 1024), (2300, 1024, 4096), (21984, 1024, 1024)])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+def test_gemm_tile_variants(N, mode, M, Nn, K, epi):
+    """Every tile form (vggt_tune VGGT_TUNE_GEMM_TILE) on shapes that exercise
+    the ring's prologue/tail (K/32 = 3, 32, 128), ragged M and N % 256 != 0."""
+    prev = N.tune(N.TUNE_GEMM_TILE, mode)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(M + Nn + K + epi)
+        a = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+        w = (torch.randn(Nn, K, device="cuda", generator=g) * K ** -0.5
+             + torch.arange(Nn, device="cuda")[:, None] * 1e-3).to(torch.bfloat16)
+        b = torch.randn(Nn, device="cuda", generator=g).to(torch.bfloat16).float()
+        refb = (a.float() @ w.float().t() + b).to(torch.bfloat16).float()
+        if epi == N.EPI_RESID_F32:
+            x0 = torch.randn(M, Nn, device="cuda", generator=g)
+            gam = torch.rand(Nn, device="cuda", generator=g)
+            x = x0.clone()
+            N.gemm_bf16(a, w, b, x, epi, gamma=gam)
+            assert _rel(x, x0 + gam * refb) < 4e-3
+        else:
+            out = torch.full((M + 1, Nn), 7.0, device="cuda", dtype=torch.bfloat16)
+            N.gemm_bf16(a, w, b, out[:M], epi)
+            r = F.gelu(refb) if epi == N.EPI_GELU_BF16 else refb
+            assert _rel(out[:M], r) < 6e-3
+            assert (out[M] == 7.0).all()  # no write past row M
+    finally:
+        N.tune(N.TUNE_GEMM_TILE, prev)
+
+
 def test_gemm_rejects_bad_shapes(N):
-    a = torch.zeros(64, 100, device="cuda", dtype=torch.bfloat16)
-    w = torch.zeros(128, 100, device="cuda", dtype=torch.bfloat16)
+    a = torch.zeros(64, 80, device="cuda", dtype=torch.bfloat16)
+    w = torch.zeros(128, 80, device="cuda", dtype=torch.bfloat16)
     b = torch.zeros(128, device="cuda")
     with pytest.raises(RuntimeError, match="shape"):
         N.gemm_bf16(a, w, b, torch.empty(64, 128, device="cuda", dtype=torch.bfloat16), 0)
@@ -138,6 +168,24 @@ def test_attention_vs_torch(N, D, H, batch, n):
     t = qkv.float().view(batch, n, 3, H, D).permute(2, 0, 3, 1, 4)
     ref = _ref_attn(t[0], t[1], t[2], D ** -0.5).permute(0, 2, 1, 3).reshape(batch * n, C)
     assert _rel(o, ref) < 1e-2, _rel(o, ref)
+
+
+@pytest.mark.parametrize("n", [4100, 5000, 8191])
+def test_attention_eight_wave_form(N, n):
+    """8-wave (256-query-row) workgroups, used for nq >= 4096."""
+    prev = N.tune(N.TUNE_ATTN_WAVES, 8)
+    try:
+        H, D = 2, 64
+        C = H * D
+        g = torch.Generator(device="cuda").manual_seed(n)
+        qkv = (torch.randn(n, 3 * C, device="cuda", generator=g) * 1.5).to(torch.bfloat16)
+        o = torch.zeros(n, C, device="cuda", dtype=torch.bfloat16)
+        N.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, 1, H, n, n, D, n, n, n)
+        t = qkv.float().view(1, n, 3, H, D).permute(2, 0, 3, 1, 4)
+        ref = _ref_attn(t[0], t[1], t[2], D ** -0.5).permute(0, 2, 1, 3).reshape(n, C)
+        assert _rel(o, ref) < 1e-2, _rel(o, ref)
+    finally:
+        N.tune(N.TUNE_ATTN_WAVES, prev)
 
 
 def test_attention_global_shape_rows(N):
