@@ -125,7 +125,9 @@ class AlignmentHead(nn.Module):
         if tokens.device.type != "cuda":
             raise RuntimeError("AlignmentHead: the MI355X hot path runs on HIP devices only (no CPU fallback)")
         if not self.temporal_attention:
-            raise NotImplementedError("temporal_attention=False is not part of any BASELINE configuration")
+            raise NotImplementedError("temporal_attention=False: the reference builds global_blocks but keeps aa_order="
+                                      "['frame', 'temporal'] (alignment_head.py:80, :146), so its forward fails; "
+                                      "not part of any BASELINE configuration")
         H_img, W_img = image_size
         B, S, P, Cin = tokens.shape
         C = self.embed_dim
