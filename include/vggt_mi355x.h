@@ -18,6 +18,7 @@
 #ifndef VGGT_MI355X_H
 #define VGGT_MI355X_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -213,6 +214,41 @@ int vggt_upsample_bilinear_f32(const float* x, int nimg, int hi, int wi, int C, 
  */
 int vggt_dpt_activate(const float* x, int64_t ldx, int64_t npix, int pix_per_img, int ncl, int act,
                       const float* scale, float* pts, float* conf, void* stream);
+
+/*
+ * Robust Sim(3) between two point-map sets, one per batch element:
+ * irls_sim3_umeyama + weighted_umeyama_sim3 (aligned_vggt/models/
+ * pointAligned_wrapped_vggt.py:159-305; called at :69-100).  src/dst:
+ * n points x 3 fp32 per batch element (batch strides in floats), conf_src /
+ * conf_dst: n fp32.  Points whose sqrt(conf_src*conf_dst) is below
+ * factor * (lower) median get weight 0; Huber IRLS with `delta`, at most
+ * max_iters iterations after the initial solve, stop when |dR|_F, |dt|, |ds|
+ * all < tol.  Outputs R_out [B,3,3], t_out [B,3], s_out [B] fp32, written on
+ * the stream (no host synchronisation); a batch element whose total weight
+ * is < 1e-6 (the reference raises ValueError) gets NaN outputs.
+ * conf_dst == NULL: conf_src holds the weights themselves; factor <= 0: no
+ * confidence threshold; max_iters == 0 with both is weighted_umeyama_sim3
+ * (pointAligned_wrapped_vggt.py:159-219).
+ * workspace: >= vggt_irls_workspace_bytes(B), 16-B aligned, device memory.
+ */
+size_t vggt_irls_workspace_bytes(int B);
+int vggt_irls_sim3(const float* src, int64_t src_bs, const float* dst, int64_t dst_bs, const float* conf_src,
+                   int64_t cs_bs, const float* conf_dst, int64_t cd_bs, int B, int64_t n, float factor, float delta,
+                   int max_iters, float tol, float* R_out, float* t_out, float* s_out, void* workspace,
+                   size_t ws_bytes, void* stream);
+
+/*
+ * out[b, i] = T_b[:3,:3] (scale_b * pts[b, i]) + T_b[:3,3] for n points (x,y,z)
+ * per batch element; T: [B,4,4] fp32 device, scale: [B] device or NULL.
+ * apply_sim3_alignment_on_point_maps (aligned_vggt/utils/alignment.py:491-526)
+ * and the point transform of featureAligned_vggt.py:200-206.  In place allowed.
+ */
+int vggt_sim3_points(const float* pts, int64_t p_bs, int B, int64_t n, const float* T, const float* scale, float* out,
+                     int64_t o_bs, void* stream);
+
+/* x[b, i] *= scale[b] (i < n) in place; scale: [B] device (depth *= chunk scale,
+ * featureAligned_vggt.py:171; pointAligned_wrapped_vggt.py:130-132). */
+int vggt_scale_f32(float* x, int64_t bs, int B, int64_t n, const float* scale, void* stream);
 
 #ifdef __cplusplus
 }

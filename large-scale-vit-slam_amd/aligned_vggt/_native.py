@@ -47,6 +47,10 @@ _SIGS = {
                         _i64, _vp, _i, _vp],
     "vggt_upsample_bilinear_f32": [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp],
     "vggt_dpt_activate": [_vp, _i64, _i64, _i, _i, _i, _vp, _vp, _vp, _vp],
+    "vggt_irls_sim3": [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i, _i64, _f, _f, _i, _f, _vp, _vp, _vp, _vp,
+                       ctypes.c_size_t, _vp],
+    "vggt_sim3_points": [_vp, _i64, _i, _i64, _vp, _vp, _vp, _i64, _vp],
+    "vggt_scale_f32": [_vp, _i64, _i, _i64, _vp, _vp],
 }
 
 _lib = None
@@ -70,6 +74,8 @@ def lib() -> ctypes.CDLL:
             fn.argtypes = argt
             fn.restype = ctypes.c_int
         L.vggt_version.restype = ctypes.c_char_p
+        L.vggt_irls_workspace_bytes.argtypes = [_i]
+        L.vggt_irls_workspace_bytes.restype = ctypes.c_size_t
         _lib = L
     return _lib
 
@@ -289,3 +295,66 @@ def dpt_activate(x: torch.Tensor, npix: int, ppi: int, ncl: int, act: int, scale
     _dev(x, "dpt_activate")
     rc = lib().vggt_dpt_activate(_p(x), _ld(x), npix, ppi, ncl, act, _p(scale), _p(pts), _p(conf), _stream())
     _check(rc, "vggt_dpt_activate")
+
+
+def _bstride(t: torch.Tensor, per_batch: int) -> int:
+    """Batch stride (elements) of a tensor whose first dim is the batch and
+    whose per-batch block of ``per_batch`` elements is contiguous."""
+    if t.shape[0] > 1:
+        return t.stride(0)
+    return per_batch
+
+
+def irls_sim3(src: torch.Tensor, dst: torch.Tensor, conf_src: torch.Tensor, conf_dst: torch.Tensor,
+              conf_threshold_factor: float = 0.5, delta: float = 0.1, max_iters: int = 20, tol: float = 1e-9):
+    """Batched irls_sim3_umeyama (pointAligned_wrapped_vggt.py:225-305) on the
+    GPU.  src/dst: (B, ..., 3) fp32, conf_*: (B, ...) fp32 with the same point
+    count; every per-batch block contiguous.  Returns device tensors R (B,3,3),
+    t (B,3), s (B,) without synchronising the host."""
+    _dev(src, "irls_sim3")
+    B = src.shape[0]
+    n = src[0].numel() // 3
+    for t_, per in ((src, 3 * n), (dst, 3 * n), (conf_src, n)) + (((conf_dst, n),) if conf_dst is not None else ()):
+        assert t_.dtype == torch.float32 and t_.shape[0] == B and t_[0].numel() == per and t_[0].is_contiguous(), \
+            "irls_sim3: (B, ..., 3) / (B, ...) fp32 inputs with contiguous per-batch blocks"
+    L = lib()
+    ws_bytes = int(L.vggt_irls_workspace_bytes(B))
+    ws = torch.empty((ws_bytes + 15) // 16 * 16, dtype=torch.uint8, device=src.device)
+    R = torch.empty(B, 3, 3, device=src.device)
+    t = torch.empty(B, 3, device=src.device)
+    s = torch.empty(B, device=src.device)
+    rc = L.vggt_irls_sim3(_p(src), _bstride(src, 3 * n), _p(dst), _bstride(dst, 3 * n), _p(conf_src),
+                          _bstride(conf_src, n), _p(conf_dst), _bstride(conf_dst, n) if conf_dst is not None else 0, B, n, float(conf_threshold_factor),
+                          float(delta), int(max_iters), float(tol), _p(R), _p(t), _p(s), _p(ws), ws.numel(), _stream())
+    _check(rc, "vggt_irls_sim3")
+    return R, t, s
+
+
+def sim3_points(pts: torch.Tensor, T: torch.Tensor, scale: Optional[torch.Tensor], out: Optional[torch.Tensor] = None):
+    """out = T[:3,:3] (scale * pts) + T[:3,3] per batch element; pts (B, ..., 3)
+    fp32 with contiguous per-batch blocks, T (B,4,4), scale (B,) or None."""
+    _dev(pts, "sim3_points")
+    B = pts.shape[0]
+    n = pts[0].numel() // 3
+    assert pts.dtype == torch.float32 and pts[0].is_contiguous()
+    T = T.to(device=pts.device, dtype=torch.float32).contiguous()
+    if scale is not None:
+        scale = scale.to(device=pts.device, dtype=torch.float32).reshape(B).contiguous()
+    if out is None:
+        out = torch.empty_like(pts)
+    rc = lib().vggt_sim3_points(_p(pts), _bstride(pts, 3 * n), B, n, _p(T), _p(scale), _p(out), _bstride(out, 3 * n),
+                                _stream())
+    _check(rc, "vggt_sim3_points")
+    return out
+
+
+def scale_(x: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    """x[b] *= scale[b] in place (fp32, contiguous per-batch blocks)."""
+    _dev(x, "scale_f32")
+    B = x.shape[0]
+    n = x[0].numel()
+    assert x.dtype == torch.float32 and x[0].is_contiguous()
+    scale = scale.to(device=x.device, dtype=torch.float32).reshape(B).contiguous()
+    rc = lib().vggt_scale_f32(_p(x), _bstride(x, n), B, n, _p(scale), _stream())
+    _check(rc, "vggt_scale_f32")
+    return x

@@ -410,12 +410,12 @@ extern "C" int vggt_gemm_bf16(const void* A, int64_t lda, const void* W, int64_t
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* w = (const bf16_t*)W;
   // Tile choice (vggt_tune VGGT_TUNE_GEMM_TILE): 0 the 128x128 form, 1 the
-  // 256x256 ring, 2 the 256x128 ring.  Auto (-1): the 256x256 ring for the wide
-  // projections (N >= 2048: qkv, fc1 -- measured 7-14% faster on the aggregator
-  // shapes), the 128x128 form for N = 1024 (proj, fc2), where 256x256 tiles
-  // leave the last of only ~1.3 rounds of workgroups mostly idle.
+  // 256x256 ring, 2 the 256x128 ring.  Auto (-1): the 256x256 ring for the MLP
+  // up-projection (N >= 4096: fc1, 256 vs 278 us in the aggregator run r1i), the
+  // 128x128 form elsewhere (qkv N = 3072: 154 vs 165 us; N = 1024 proj / fc2,
+  // where 256x256 tiles leave the last of only ~1.3 rounds of workgroups idle).
   int mode = g_vggt_gemm_tile;
-  if (mode < 0) mode = (N >= 2048 && N % 256 == 0 && M >= 1024) ? 1 : 0;
+  if (mode < 0) mode = (N >= 4096 && N % 256 == 0 && M >= 1024) ? 1 : 0;
   if (mode == 0 && K % BK) mode = 2;     // the 128x128 form steps K by 64
   if (mode == 1 && N % 256) mode = 2;
   // per-lane 32-bit DMA offsets span one 256-row panel

@@ -44,6 +44,21 @@ def extract(ref: str, relpath: str, names):
     return {n: g[n] for n in names}
 
 
+def extract_methods(ref: str, relpath: str, cls: str, names):
+    """Exec the named methods of a reference class as free functions taking
+    an explicit ``self`` (the class's own base, e.g. torchmetrics.Metric, is
+    not needed by these bodies: they only read/write plain attributes)."""
+    src = open(os.path.join(ref, relpath)).read()
+    tree = ast.parse(src)
+    (c,) = [n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == cls]
+    keep = [n for n in c.body if isinstance(n, ast.FunctionDef) and n.name in names]
+    assert {n.name for n in keep} == set(names)
+    mod = ast.Module(body=keep, type_ignores=[])
+    g = {"torch": torch, "np": np, "Tuple": Tuple, "__name__": "golden_extract"}
+    exec(compile(mod, relpath, "exec"), g)
+    return {n: g[n] for n in names}
+
+
 def save(name, **arrays):
     out = {}
     for k, v in arrays.items():
@@ -148,6 +163,113 @@ def gen_irls(ref):
     save("irls_sim3", src=src, dst=dst, conf_src=cs, conf_dst=cd, r=r, t=t, s=np.array(float(s)))
 
 
+def gen_irls_batch(ref):
+    """Three independent problems with 5% gross outliers and ragged confidences
+    (the batched GPU kernel solves them in one call)."""
+    fns = extract(ref, "aligned_vggt/models/pointAligned_wrapped_vggt.py",
+                  ["weighted_umeyama_sim3", "irls_sim3_umeyama"])
+    g = torch.Generator().manual_seed(33)
+    out = {}
+    for b in range(3):
+        src = torch.randn(3, 24, 32, 3, generator=g) * 4 + torch.tensor([0.0, 0.0, 10.0])
+        ang = 0.2 + 0.3 * b
+        ax = F.normalize(torch.randn(3, generator=g), dim=0)
+        K = torch.tensor([[0, -ax[2], ax[1]], [ax[2], 0, -ax[0]], [-ax[1], ax[0], 0]])
+        R = torch.eye(3) + np.sin(ang) * K + (1 - np.cos(ang)) * K @ K
+        dst = (0.5 + 0.4 * b) * src @ R.T + torch.randn(3, generator=g)
+        dst = dst + 0.02 * torch.randn(dst.shape, generator=g)
+        out_mask = torch.rand(src.shape[:-1], generator=g) < 0.05
+        dst[out_mask] += torch.randn(int(out_mask.sum()), 3, generator=g) * 5
+        cs = 1 + torch.rand(src.shape[:-1], generator=g) * 4
+        cd = 1 + torch.rand(src.shape[:-1], generator=g) * 4
+        cs[0, :4] = 1.0  # a low-confidence band below the median threshold
+        r, t, s = fns["irls_sim3_umeyama"](src, dst, cs, cd)
+        out.update({f"src{b}": src, f"dst{b}": dst, f"cs{b}": cs, f"cd{b}": cd, f"r{b}": r, f"t{b}": t,
+                    f"s{b}": np.array(float(s))})
+    save("irls_sim3_batch", **out)
+
+
+def gen_trajectory_metrics(ref):
+    """ATE / RPE (eval/trajectory_metrics.py:28-77, :154-223): the update /
+    compute bodies run on plain attribute holders."""
+    from types import SimpleNamespace
+    ate = extract_methods(ref, "eval/trajectory_metrics.py", "AbsoluteTrajectoryError", ["update", "compute"])
+    rpe = extract_methods(ref, "eval/trajectory_metrics.py", "RelativePoseError", ["update", "compute"])
+    g = torch.Generator().manual_seed(7)
+    N = 40
+    yaw = torch.cumsum(torch.randn(N, generator=g) * np.deg2rad(2.0), 0)
+    gt = torch.eye(4).repeat(N, 1, 1)
+    gt[:, 0, 0] = torch.cos(yaw)
+    gt[:, 0, 2] = torch.sin(yaw)
+    gt[:, 2, 0] = -torch.sin(yaw)
+    gt[:, 2, 2] = torch.cos(yaw)
+    gt[:, :3, 3] = torch.cumsum(torch.stack([torch.sin(yaw), torch.zeros(N), torch.cos(yaw)], -1), 0)
+    pred = gt.clone()
+    dyaw = torch.randn(N, generator=g) * 0.02
+    c, s_ = torch.cos(dyaw), torch.sin(dyaw)
+    Rz = torch.eye(4).repeat(N, 1, 1)
+    Rz[:, 0, 0], Rz[:, 0, 1], Rz[:, 1, 0], Rz[:, 1, 1] = c, -s_, s_, c
+    pred = pred @ Rz
+    pred[:, :3, 3] += torch.randn(N, 3, generator=g) * 0.05
+    out = {"gt": gt, "pred": pred}
+    for det in (False, True):
+        st = SimpleNamespace(errors=torch.tensor([], dtype=torch.float32),
+                             per_dim_errors=torch.tensor([], dtype=torch.float32), detailed=det)
+        ate["update"](st, pred[:25], gt[:25])
+        ate["update"](st, pred[25:], gt[25:])
+        r = ate["compute"](st)
+        for k, v in r.items():
+            out[f"ate_{int(det)}_{k}"] = np.array(v)
+    for delta in (1, 3):
+        st = SimpleNamespace(trans_errors=torch.tensor([], dtype=torch.float32),
+                             rot_errors=torch.tensor([], dtype=torch.float32), detailed=True, delta=delta)
+        rpe["update"](st, pred, gt)
+        rpe["update"](st, pred[:2], gt[:2])  # N <= delta for delta 3: ignored
+        for k, v in rpe["compute"](st).items():
+            out[f"rpe_{delta}_{k}"] = np.array(v)
+    save("trajectory_metrics", **out)
+
+
+def gen_scale_alignment(ref):
+    """GT-based output alignment (aligned_vggt/utils/alignment.py:131-323)."""
+    fns = extract(ref, "aligned_vggt/utils/alignment.py",
+                  ["scale_lse_solver", "per_frame_scale_alignment_from_poses", "per_chunk_scale_alignment_from_poses",
+                   "scale_alignment_from_poses", "scale_align_from_depths"])
+    g = torch.Generator().manual_seed(17)
+    B, S, H, W = 2, 6, 5, 7
+
+    def preds():
+        gg = torch.Generator().manual_seed(18)
+        return {"pose_enc": torch.randn(B, S, 9, generator=gg), "depth": torch.rand(B, S, H, W, 1, generator=gg) + 0.5,
+                "depth_conf": torch.rand(B, S, H, W, generator=gg) + 1,
+                "world_points": torch.randn(B, S, H, W, 3, generator=gg)}
+    extr = torch.randn(B, S, 3, 4, generator=g)
+    depths = torch.rand(B, S, H, W, generator=g) * 3 + 0.2
+    mask = torch.rand(B, S, H, W, generator=g) > 0.2
+    out = {"extr": extr, "depths": depths, "mask": mask}
+    p0 = preds()
+    out.update({"in_" + k: v for k, v in p0.items()})
+    for name, call in (("scale_poses", lambda p: fns["scale_alignment_from_poses"](p, {"extrinsics": extr})),
+                       ("scale_poses_w3", lambda p: fns["scale_alignment_from_poses"](p, {"extrinsics": extr}, 3)),
+                       ("frame_scale", lambda p: fns["per_frame_scale_alignment_from_poses"](p, {"extrinsics": extr})),
+                       ("depth_scale", lambda p: fns["scale_align_from_depths"](
+                           p, {"depths": depths[..., None], "point_masks": mask}))):
+        p = preds()
+        call(p)
+        for k in ("pose_enc", "depth", "world_points"):
+            out[f"{name}_{k}"] = p[k]
+        sc = p["alignment_scales"]
+        out[f"{name}_scales"] = np.array([np.asarray(v, dtype=np.float64) for v in sc], dtype=np.float64)
+    # per chunk: lists of chunks
+    pc = preds()
+    chunked = {k: [v[:, :3].clone(), v[:, 3:].clone()] for k, v in pc.items()}
+    fns["per_chunk_scale_alignment_from_poses"](chunked, {"extrinsics": [extr[:, :3], extr[:, 3:]]})
+    for k in ("pose_enc", "depth", "world_points"):
+        out[f"chunk_scale_{k}"] = torch.cat(chunked[k], 1)
+    out["chunk_scale_scales"] = torch.stack(chunked["alignment_scales_per_chunk"])
+    save("scale_alignment", **out)
+
+
 def gen_small_fns(ref):
     mr = extract(ref, "aligned_vggt/models/featureAligned_vggt.py", ["merge_results"])["merge_results"]
     se = extract(ref, "aligned_vggt/heads/alignment_head.py", ["slice_expand_and_flatten"])["slice_expand_and_flatten"]
@@ -213,13 +335,21 @@ def gen_dinov2():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default=None, help="comma-separated generator names (e.g. irls_batch,trajectory_metrics)")
     a = ap.parse_args()
+    if a.only:
+        for n in a.only.split(","):
+            globals()["gen_" + n](a.ref) if n != "dinov2" else gen_dinov2()
+        return
     gen_rope(a.ref)
     gen_gated_update(a.ref)
     gen_chunks(a.ref)
     gen_geometry(a.ref)
     gen_alignment(a.ref)
     gen_irls(a.ref)
+    gen_irls_batch(a.ref)
+    gen_trajectory_metrics(a.ref)
+    gen_scale_alignment(a.ref)
     gen_small_fns(a.ref)
     gen_dinov2()
 

@@ -82,3 +82,26 @@ def test_pose_roundtrip_known_answer():
     enc = torch.cat([torch.randn(2, 5, 3, generator=g), q], dim=-1)
     np.testing.assert_allclose(O.extri_to_pose_encoding(O.pose_encoding_to_extri(enc))[..., :3].numpy(),
                                enc[..., :3].numpy(), atol=1e-6)
+
+
+def test_irls_sim3_oracle_matches_reference(golden):
+    from oracle import alignment_oracle as AO
+    g = golden("irls_sim3")
+    r, t, s = AO.irls_sim3_umeyama(*(torch.from_numpy(g[k]) for k in ("src", "dst", "conf_src", "conf_dst")))
+    np.testing.assert_allclose(r.numpy(), g["r"], atol=1e-5)
+    np.testing.assert_allclose(t.numpy(), g["t"], atol=1e-5)
+    np.testing.assert_allclose(float(s), g["s"], rtol=1e-5)
+    gb = golden("irls_sim3_batch")
+    for b in range(3):
+        r, t, s = AO.irls_sim3_umeyama(*(torch.from_numpy(gb[f"{k}{b}"]) for k in ("src", "dst", "cs", "cd")))
+        np.testing.assert_allclose(r.numpy(), gb[f"r{b}"], atol=1e-5)
+        np.testing.assert_allclose(t.numpy(), gb[f"t{b}"], atol=1e-4)
+        np.testing.assert_allclose(float(s), gb[f"s{b}"], rtol=1e-5)
+
+
+def test_sim3_point_map_oracle_matches_reference(golden):
+    from oracle import alignment_oracle as AO
+    g = golden("alignment_utils")
+    out = AO.apply_sim3_alignment_on_point_maps(torch.from_numpy(g["pm"]), torch.from_numpy(g["T"]),
+                                                torch.from_numpy(g["sc"]))
+    np.testing.assert_allclose(out.numpy(), g["pm_out"], rtol=1e-6, atol=1e-6)
