@@ -206,13 +206,26 @@ def main():
                          "unit": "TFLOP/s",
                          "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4) if attn_tflops else None,
                          "avg_launch_ms": round(attn_ms, 4) if attn_ms else None,
-                         "flops_per_launch": fl["global_attn_launch"], "traffic": None},
+                         "flops_per_launch": fl["global_attn_launch"], "traffic": _pmc_traffic()},
         }
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(args.cpu_threads)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _pmc_traffic():
+    """HBM bytes per global-attention launch from the committed PMC summary
+    (profiles/attn_traffic.json, written by scripts/pmc_traffic.py from two
+    separate `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` passes of this
+    same bench command; FETCH_SIZE x2 per the gfx950 correction), or None."""
+    p = os.path.join(ROOT, "profiles", "attn_traffic.json")
+    try:
+        with open(p) as fh:
+            return json.load(fh)["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def bench_full(args, world, rank, dev):

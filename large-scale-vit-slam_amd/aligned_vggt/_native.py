@@ -86,6 +86,7 @@ def version() -> str:
 
 TUNE_GEMM_TILE = 1
 TUNE_ATTN_WAVES = 2
+TUNE_ATTN_VARIANT = 3
 
 
 def tune(knob: int, value: int) -> int:

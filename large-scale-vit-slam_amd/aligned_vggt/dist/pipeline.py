@@ -33,33 +33,30 @@ from typing import Dict, List, Optional
 import torch
 import torch.distributed as dist
 
-from ..utils.data import chunk_batch, convertDictListsToTensors, generate_chunks, moveDictListItemToCPU
+from ..utils.data import alignAndConvertOutputs, chunk_batch, generate_chunks, moveDictListItemToCPU
 
 
 def apply_sequence_to_model(batch: dict, model, chunk_width, num_overlap, sample_mode: str = "chunk_overlap",
                             alignment_type: Optional[str] = None) -> dict:
-    """training_metrics.py:616-659 (no_grad inference chunk loop)."""
+    """training_metrics.py:616-659 (no_grad inference chunk loop): chunk the
+    sequence, thread ``context`` through the model, offload older chunk
+    outputs to host memory, then align (GT-based, optional) and merge the
+    per-chunk lists into overlap-free tensors in place (data.py:108-153).
+    ``batch`` gains the merged ground-truth tensors, as in the reference."""
     S = batch["images"].shape[1]
     chunk_width = chunk_width[0] if isinstance(chunk_width, (list, tuple)) else chunk_width
     num_overlap = num_overlap[0] if isinstance(num_overlap, (list, tuple)) else num_overlap
     indices = generate_chunks(S, sample_mode, chunk_width, num_overlap)
     chunked = chunk_batch(batch, indices)
-    preds = None
+    predictions = None
     for i in range(len(indices)):
-        gt = chunked["extrinsics"][i] if sample_mode in ("chunk_gt", "two_chunks") and "extrinsics" in chunked else None
+        gt = chunked["extrinsics"][i] if sample_mode in ("chunk_gt", "two_chunks") else None
         with torch.no_grad():
-            preds = model(chunked["images"][i], num_overlap, preds, gt_poses=gt)
-        moveDictListItemToCPU(preds, -2)
-    moveDictListItemToCPU(preds, -1)
-    if alignment_type not in (None, "null", "none"):
-        raise NotImplementedError("GT-based output alignment (data.py:108-153) is evaluation post-processing, "
-                                  "out of scope for the hot path (SURVEY.md §2)")
-    out = {}
-    convertDictListsToTensors(preds, num_overlap if len(indices) > 1 else 0, out)
-    for k in ("chunk_sim3_alignment_enc", "frame_se3_alignment_enc"):
-        if k in preds:
-            out[k] = preds[k]
-    return out
+            predictions = model(chunked["images"][i], num_overlap, predictions, gt_poses=gt)
+        moveDictListItemToCPU(predictions, -2)
+    moveDictListItemToCPU(predictions, -1)
+    alignAndConvertOutputs(predictions, batch, chunked, alignment_type, chunk_width, num_overlap)
+    return predictions
 
 
 def _overlap_of(S: int, num_overlap: int) -> int:

@@ -14,6 +14,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import _native as N
 from ..backbone.aggregator import Aggregator
 from ..backbone.camera_head import CameraHead
 from ..backbone.dpt_head import DPTHead
@@ -152,7 +153,7 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
                     predictions["memory_tokens"] = context["memory_tokens"]
 
         if self.depth_head is not None:
-            depth = enc["depth"] * chunk_scale.view(B, 1, 1, 1, 1)
+            depth = N.scale_(enc["depth"], chunk_scale.reshape(B))  # in place, featureAligned_vggt.py:171
             depth_conf = enc["depth_conf"]
             if context is None:
                 predictions["depth"] = [depth]
@@ -171,10 +172,8 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
                     pt = pt @ point_identity_alignment.view(B, 1, 4, 4)
                 else:
                     pt = point_identity_alignment.view(B, 1, 4, 4)
-                pts3d = pts3d * chunk_scale.view(B, 1, 1, 1, 1)
-                R = pt[:, 0, :3, :3]
-                t = pt[:, 0, :3, 3]
-                pts3d = (pts3d.reshape(B, -1, 3) @ R.transpose(-1, -2) + t[:, None]).view(B, S, H, W, 3)
+                # featureAligned_vggt.py:200-206: scale, then the SE(3) of pt, one HIP pass
+                pts3d = N.sim3_points(pts3d.contiguous(), pt[:, 0], chunk_scale.reshape(B))
             if context is None:
                 predictions["world_points"] = [pts3d]
                 predictions["world_points_conf"] = [pts3d_conf]

@@ -61,6 +61,41 @@ def moveDictListItemToCPU(chunked_dict: dict, itemIndex: int) -> None:
                 v[itemIndex] = v[itemIndex].cpu()
 
 
+def alignAndConvertOutputs(predictions: dict, batch: dict, chunked_batch: dict, alignment_type: str, seq_width: int,
+                           overlap: int) -> None:
+    """data.py:108-153: optional GT-based alignment of the merged sequence
+    outputs (evaluation post-processing; aligned_vggt/utils/alignment.py),
+    with the per-chunk lists converted to overlap-free tensors in place."""
+    from . import alignment as A
+    if alignment_type == "per_chunk_scale_from_poses":
+        A.per_chunk_scale_alignment_from_poses(predictions, chunked_batch)
+        convertDictListsToTensors(chunked_batch, overlap, batch)
+        convertDictListsToTensors(predictions, overlap)
+        return
+    convertDictListsToTensors(chunked_batch, overlap, batch)
+    convertDictListsToTensors(predictions, overlap)
+    if alignment_type == "scale_from_fc_poses":
+        A.scale_alignment_from_poses(predictions, batch, seq_width)
+    elif alignment_type == "scale_from_poses":
+        A.scale_alignment_from_poses(predictions, batch)
+    elif alignment_type == "per_frame_scale_from_poses":
+        A.per_frame_scale_alignment_from_poses(predictions, batch)
+    elif alignment_type == "scale_from_depths":
+        if "depth" not in predictions:
+            raise ValueError("scale_from_depths alignment requires depth head to be enabled.")
+        A.scale_align_from_depths(predictions, batch)
+    elif alignment_type == "sim3_from_poses":
+        A.umeyama_alignment_from_poses(predictions, batch, seq_width)
+    elif alignment_type == "sim3_from_points":
+        if "world_points" not in predictions:
+            raise ValueError("sim3_from_points alignment requires point head to be enabled.")
+        T, sc = A.umeyama_alignment_from_points(predictions["world_points"][:, :seq_width],
+                                                predictions["world_points_conf"][:, :seq_width],
+                                                batch["world_points"][:, :seq_width],
+                                                batch["point_masks"][:, :seq_width], confidence_threshold=50.0)
+        A.apply_sim3_alignment_on_dict(predictions, batch["images"].shape[-2:], T, sc)
+
+
 def generate_chunks(num_frames: int, mode: str, seq_width: int, overlap: int) -> List[List[int]]:
     """data.py:155-207."""
     indices = []

@@ -88,7 +88,12 @@ __device__ __forceinline__ int v_swz(int row, int chunk) {
   else return chunk ^ ((row & 3) << 2);
 }
 
-template <int D, int NW>
+// VAR (schedule variants, A/B-tested through vggt_tune): bit 0 = all K
+// fragment reads before the QK^T MFMAs, bit 1 = four-chain row max, bit 2 =
+// four partial row sums, bit 3 = row sums on the matrix core (an all-ones
+// V^T block times P^T: 4 extra MFMAs per tile replace 32 VALU adds per lane;
+// the sum is then over the bf16-rounded P that also feeds P.V).
+template <int D, int NW, int VAR>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
   constexpr int BQ = NW * 32;            // query rows per workgroup (32 per wave)
   constexpr int ROWB = D * 2;            // bytes per K/V row in LDS
@@ -177,6 +182,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
   for (int i = 0; i < NDB; ++i) o[i] = f32x16{};
   float m_run = -INFINITY, l_run = 0.f;
+  f32x16 lsum = f32x16{};  // VAR & 8: every row of the ones-block product holds l[q]
   const float c = a.c;
   const int nt = (a.nk + BKV - 1) / BKV;
 
@@ -185,13 +191,30 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
     const char* base = smem + BUF * 2 * TILEB;
     // ---- S^T = K . Q^T for two 32-key blocks
     f32x16 s[2];
+    if constexpr (VAR & 1) {
+      // all K fragment reads first, then the two 32-key accumulator chains
+      // interleaved (no MFMA waits on a just-issued LDS read)
+      bf16x8 kf[2][NKS];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      s[kb] = f32x16{};
+      for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        const bf16x8 kf = *(const bf16x8*)(base + ka[ks] + kb * 32 * ROWB);
-        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kb], 0, 0, 0);
+        for (int kb = 0; kb < 2; ++kb) kf[kb][ks] = *(const bf16x8*)(base + ka[ks] + kb * 32 * ROWB);
+      s[0] = f32x16{};
+      s[1] = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+          s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][ks], qf[ks], s[kb], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        s[kb] = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          const bf16x8 kf = *(const bf16x8*)(base + ka[ks] + kb * 32 * ROWB);
+          s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kb], 0, 0, 0);
+        }
       }
     }
     const int kv0 = t * BKV;
@@ -205,11 +228,28 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
         }
     }
     // ---- row max (lane-partial over 32 keys, then the partner half)
-    float mx = fmaxf(s[0][0], s[0][1]);  // chained as v_max3_f32 (built with -fno-honor-nans)
+    float mx;
+    if constexpr (VAR & 2) {
+      // four independent v_max3 chains (built with -fno-honor-nans), merged:
+      // dependency depth 5 instead of 16
+      float mc[4];
 #pragma unroll
-    for (int r = 2; r < 16; r += 2) mx = fmaxf(fmaxf(mx, s[0][r]), s[0][r + 1]);
+      for (int cc = 0; cc < 4; ++cc) {
+        const f32x16& sv = s[cc >> 1];
+        const int r0 = (cc & 1) * 8;
+        float m = fmaxf(sv[r0], sv[r0 + 1]);
 #pragma unroll
-    for (int r = 0; r < 16; r += 2) mx = fmaxf(fmaxf(mx, s[1][r]), s[1][r + 1]);
+        for (int r = r0 + 2; r < r0 + 8; r += 2) m = fmaxf(fmaxf(m, sv[r]), sv[r + 1]);
+        mc[cc] = m;
+      }
+      mx = fmaxf(fmaxf(mc[0], mc[1]), fmaxf(mc[2], mc[3]));
+    } else {
+      mx = fmaxf(s[0][0], s[0][1]);  // one v_max3 chain
+#pragma unroll
+      for (int r = 2; r < 16; r += 2) mx = fmaxf(fmaxf(mx, s[0][r]), s[0][r + 1]);
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) mx = fmaxf(fmaxf(mx, s[1][r]), s[1][r + 1]);
+    }
     {
       const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
       mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * c;
@@ -219,11 +259,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
       const float m_new = fmaxf(m_run, mx);
       const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
       m_run = m_new;
-      l_run *= alpha;
+      if constexpr (VAR & 8) lsum *= alpha;
+      else l_run *= alpha;
 #pragma unroll
       for (int db = 0; db < NDB; ++db) o[db] *= alpha;
     }
-    float rs = 0.f;
+    float rs[4] = {0.f, 0.f, 0.f, 0.f};  // four partial row sums (short add chains)
     bf16x8 pf[2][2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
@@ -232,10 +273,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float p = __builtin_amdgcn_exp2f(fmaf(s[kb][8 * ss + j], c, -m_run));
-          rs += p;
+          if constexpr (!(VAR & 8)) rs[(VAR & 4) ? 2 * kb + ss : 0] += p;
           pf[kb][ss][j] = (__bf16)p;
         }
-    l_run += rs;
+    if constexpr (!(VAR & 8)) l_run += (rs[0] + rs[1]) + (rs[2] + rs[3]);
     // ---- O^T += V^T . P^T
 #pragma unroll
     for (int db = 0; db < NDB; ++db)
@@ -250,6 +291,15 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
           const bf16x8 vf = __builtin_bit_cast(bf16x8, (s16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
           o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kb][ss], o[db], 0, 0, 0);
         }
+    if constexpr (VAR & 8) {
+      bf16x8 ones;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) lsum = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[kb][ss], lsum, 0, 0, 0);
+    }
   };
 
   stage(0, 0);
@@ -268,7 +318,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
   }
 
   // ---- epilogue: normalise, O[q][d] bf16
-  {
+  if constexpr (VAR & 8) {
+    l_run = lsum[0];
+  } else {
     const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run), __float_as_uint(l_run), false, false);
     l_run = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
   }
@@ -308,12 +360,21 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
   const int nw = (g_vggt_attn_waves == 8 && nq >= 4096) ? 8 : 4;
   const int nwg = ((nq + nw * 32 - 1) / (nw * 32)) * heads * batch;
   hipStream_t s = (hipStream_t)stream;
-  if (nw == 8) {
-    if (D == 64) attn_fwd_kernel<64, 8><<<nwg, 512, 0, s>>>(a);
-    else attn_fwd_kernel<128, 8><<<nwg, 512, 0, s>>>(a);
-  } else {
-    if (D == 64) attn_fwd_kernel<64, 4><<<nwg, 256, 0, s>>>(a);
-    else attn_fwd_kernel<128, 4><<<nwg, 256, 0, s>>>(a);
+  switch ((D == 64 ? 0 : 32) + (nw == 8 ? 16 : 0) + (g_vggt_attn_variant & 15)) {
+#define VGGT_ATTN_CASE(DD, NWW, V) \
+  case (DD == 64 ? 0 : 32) + (NWW == 8 ? 16 : 0) + V: attn_fwd_kernel<DD, NWW, V><<<nwg, NWW * 64, 0, s>>>(a); break;
+#define VGGT_ATTN_CASES(DD, NWW)                                                                            \
+  VGGT_ATTN_CASE(DD, NWW, 0) VGGT_ATTN_CASE(DD, NWW, 1) VGGT_ATTN_CASE(DD, NWW, 2) VGGT_ATTN_CASE(DD, NWW, 3)  \
+  VGGT_ATTN_CASE(DD, NWW, 4) VGGT_ATTN_CASE(DD, NWW, 5) VGGT_ATTN_CASE(DD, NWW, 6) VGGT_ATTN_CASE(DD, NWW, 7)  \
+  VGGT_ATTN_CASE(DD, NWW, 8) VGGT_ATTN_CASE(DD, NWW, 9) VGGT_ATTN_CASE(DD, NWW, 10) VGGT_ATTN_CASE(DD, NWW, 11) \
+  VGGT_ATTN_CASE(DD, NWW, 12) VGGT_ATTN_CASE(DD, NWW, 13) VGGT_ATTN_CASE(DD, NWW, 14) VGGT_ATTN_CASE(DD, NWW, 15)
+    VGGT_ATTN_CASES(64, 4)
+    VGGT_ATTN_CASES(64, 8)
+    VGGT_ATTN_CASES(128, 4)
+    VGGT_ATTN_CASES(128, 8)
+#undef VGGT_ATTN_CASES
+#undef VGGT_ATTN_CASE
+    default: return VGGT_ERR_UNSUPPORTED;
   }
   HIP_LAUNCH_CHECK();
   return VGGT_OK;

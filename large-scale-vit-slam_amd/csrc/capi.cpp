@@ -16,6 +16,7 @@ int env_or(const char* name, int dflt) {
 
 int g_vggt_gemm_tile = env_or("VGGT_GEMM", -1);
 int g_vggt_attn_waves = env_or("VGGT_ATTN_WAVES", 4);
+int g_vggt_attn_variant = env_or("VGGT_ATTN_VARIANT", 3);
 
 extern "C" int vggt_tune(int knob, int value) {
   int prev;
@@ -29,6 +30,11 @@ extern "C" int vggt_tune(int knob, int value) {
       if (value != 4 && value != 8) return VGGT_ERR_UNSUPPORTED;
       prev = g_vggt_attn_waves;
       g_vggt_attn_waves = value;
+      return prev;
+    case VGGT_TUNE_ATTN_VARIANT:
+      if (value < 0 || value > 15) return VGGT_ERR_UNSUPPORTED;
+      prev = g_vggt_attn_variant;
+      g_vggt_attn_variant = value;
       return prev;
     default: return VGGT_ERR_UNSUPPORTED;
   }

@@ -10,6 +10,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "large-scale-vit-slam_amd"))
@@ -38,6 +39,9 @@ def main():
     ap.add_argument("--only", default="gemm,norm,attn")
     ap.add_argument("--gemm-modes", default="0,1,2")
     ap.add_argument("--attn-waves", default="4,8")
+    ap.add_argument("--attn-variants", default="0")
+    ap.add_argument("--rounds", type=int, default=1, help="repeat the attention sweep (A/B alternation)")
+    ap.add_argument("--warm-s", type=float, default=3.0)
     args = ap.parse_args()
     only = set(args.only.split(","))
     dev = torch.device("cuda:0")
@@ -81,13 +85,23 @@ def main():
         qkv = (torch.randn(M, 3 * C, device=dev)).bfloat16()
         o = torch.empty(M, C, device=dev, dtype=torch.bfloat16)
         q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
-        for nw, (name, batch, n) in [(w_, sh) for w_ in map(int, args.attn_waves.split(","))
-                                     for sh in (("global_attn", 1, M), ("frame_attn", 16, 1374))]:
+        # bring clocks / power to the steady state first (the first ~2 s of a
+        # cold box measure 5-20% slow)
+        t_end = time.time() + args.warm_s
+        while time.time() < t_end:
+            N.attention(q, k, v, o, 1, H, M, M, D, M, M, M)
+            torch.cuda.synchronize()
+        for rnd, var, nw, (name, batch, n) in [(r_, v_, w_, sh) for r_ in range(args.rounds)
+                                          for v_ in map(int, args.attn_variants.split(","))
+                                          for w_ in map(int, args.attn_waves.split(","))
+                                          for sh in (("global_attn", 1, M), ("frame_attn", 16, 1374))]:
             N.tune(N.TUNE_ATTN_WAVES, nw)
+            N.tune(N.TUNE_ATTN_VARIANT, var)
             us = timeit(lambda: N.attention(q, k, v, o, batch, H, n, n, D, n, n, n),
                         max(3, args.reps // 4))
-            res[f"{name}/w{nw}"] = {"us": round(us, 1), "tflops": round(4 * batch * H * n * n * D / us / 1e6, 1)}
-            print(f"{name}/w{nw}", res[f"{name}/w{nw}"], flush=True)
+            key = f"{name}/w{nw}/v{var}" + (f"/r{rnd}" if args.rounds > 1 else "")
+            res[key] = {"us": round(us, 1), "tflops": round(4 * batch * H * n * n * D / us / 1e6, 1)}
+            print(key, res[key], flush=True)
     print(json.dumps(res))
 
 

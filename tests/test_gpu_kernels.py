@@ -157,9 +157,18 @@ def _ref_attn(q, k, v, scale):
     return torch.softmax(s, -1) @ v.float()
 
 
+@pytest.mark.parametrize("variant", [3, 11, 15])
 @pytest.mark.parametrize("D,H,batch,n", [(64, 16, 3, 21), (64, 16, 2, 1374), (128, 8, 2, 1375), (64, 2, 1, 4100),
                                          (128, 2, 1, 64), (64, 1, 1, 1)])
-def test_attention_vs_torch(N, D, H, batch, n):
+def test_attention_vs_torch(N, D, H, batch, n, variant):
+    prev = N.tune(N.TUNE_ATTN_VARIANT, variant)
+    try:
+        _attention_vs_torch(N, D, H, batch, n)
+    finally:
+        N.tune(N.TUNE_ATTN_VARIANT, prev)
+
+
+def _attention_vs_torch(N, D, H, batch, n):
     C = H * D
     g = torch.Generator(device="cuda").manual_seed(n + D)
     qkv = (torch.randn(batch * n, 3 * C, device="cuda", generator=g) * 1.5).to(torch.bfloat16)
@@ -205,9 +214,18 @@ def test_attention_global_shape_rows(N):
     assert _rel(o[rows], ref) < 1e-2
 
 
-def test_attention_online_softmax_rescale(N):
+@pytest.mark.parametrize("variant", [3, 11])
+def test_attention_online_softmax_rescale(N, variant):
     """Force the running max to jump late (rule 26): one key with a huge score
     in the last tile for some rows."""
+    prev = N.tune(N.TUNE_ATTN_VARIANT, variant)
+    try:
+        _online_softmax_rescale(N)
+    finally:
+        N.tune(N.TUNE_ATTN_VARIANT, prev)
+
+
+def _online_softmax_rescale(N):
     n, H, D = 700, 2, 64
     C = H * D
     q = torch.randn(n, C, device="cuda") * 0.1

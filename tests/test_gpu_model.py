@@ -141,3 +141,53 @@ def test_feature_aligned_given_oracle_tokens(models, monkeypatch):
     assert _rel(got_ctx["chunk_sim3_alignment_enc"], ref_ctx["chunk_sim3_alignment_enc"]) < 1e-3
     for a, b in zip(got_ctx["depth"], ref_ctx["depth"]):
         assert _rel(a, b) < 1e-3
+
+
+def _synthetic_w2c(S, seed=7):
+    """Smooth synthetic trajectory (yaw random walk, ~1 unit forward per frame), w2c (1,S,3,4)."""
+    g = torch.Generator().manual_seed(seed)
+    yaw = torch.cumsum(torch.randn(S, generator=g) * 0.0087, 0)
+    c2w = torch.eye(4).repeat(S, 1, 1)
+    c2w[:, 0, 0], c2w[:, 0, 2], c2w[:, 2, 0], c2w[:, 2, 2] = yaw.cos(), yaw.sin(), -yaw.sin(), yaw.cos()
+    c2w[:, :3, 3] = torch.cumsum(torch.stack([yaw.sin(), torch.zeros(S), yaw.cos()], -1), 0)
+    return torch.linalg.inv(c2w)[:, :3, :][None]
+
+
+def test_sequence_ate_rpe_parity(models):
+    """Full-sequence evaluation (training_metrics.py:157-260 pose path): the
+    HIP model through apply_sequence_to_model (3 overlapping chunks, GT scale
+    alignment 'scale_from_poses') vs the oracle chunk loop; ATE / RPE of both
+    against the same synthetic GT trajectory must agree."""
+    m, sd = models
+    from aligned_vggt.dist.pipeline import apply_sequence_to_model
+    from aligned_vggt.eval import AbsoluteTrajectoryError, RelativePoseError, poses_c2w_from_predictions
+    from aligned_vggt.utils import alignment as A
+    from aligned_vggt.utils.synthetic import synthetic_images
+    S, w, ov, H, W = 7, 4, 2, 42, 56
+    imgs = synthetic_images(1, S, H, W, seed=12)
+    extr = _synthetic_w2c(S)
+    batch = {"images": imgs.cuda(), "extrinsics": extr.cuda()}
+    got = apply_sequence_to_model(batch, m, [w], [ov], "chunk_overlap", "scale_from_poses")
+
+    def oracle_seq(bf16):
+        ctx = None
+        for ids in O.generate_chunks(S, w, ov):
+            ctx = O.feature_aligned_forward(sd, imgs[:, ids], ov, ctx, enable_point=True, bf16=bf16)
+        pe = torch.cat([p[:, (ov if i else 0):] for i, p in enumerate(ctx["pose_enc"])], 1)
+        pred = {"pose_enc": pe}
+        A.scale_alignment_from_poses(pred, {"extrinsics": extr})
+        return pred["pose_enc"]
+
+    def metrics(pose_enc):
+        p, g = poses_c2w_from_predictions(pose_enc.cpu(), extr, (H, W))
+        ate, rpe = AbsoluteTrajectoryError(), RelativePoseError()
+        ate.update(p[0], g[0])
+        rpe.update(p[0], g[0])
+        return {**ate.compute(), **rpe.compute()}
+
+    assert got["pose_enc"].shape == (1, S, 9)
+    m_hip, m_ref, m_32 = metrics(got["pose_enc"]), metrics(oracle_seq(True)), metrics(oracle_seq(False))
+    print("hip", m_hip, "\nref bf16", m_ref, "\nref fp32", m_32)
+    for k in m_ref:
+        spread = abs(m_32[k] - m_ref[k])
+        assert abs(m_hip[k] - m_ref[k]) <= max(5e-2 * abs(m_ref[k]), 1.5 * spread) + 1e-6, (k, m_hip, m_ref, m_32)
