@@ -71,6 +71,22 @@ int vggt_gemm_bf16(const void* A, int64_t lda, const void* W, int64_t ldw, const
                    int epi, void* out, int64_t ldo, const float* gamma, float* out2, int64_t ldo2, void* stream);
 
 /*
+ * Fused attention input projection: qkv[M, 3*H*D] = bf16(A . W^T + bias), then,
+ * in the same epilogue, the q and k column blocks get the per-head LayerNorm
+ * (q_norm / k_norm: weights [D], eps; NULL weights = no norm) and RoPE
+ * (rope_mode/pos/period/cos/sin as vggt_headnorm_rope), computed in fp32 on
+ * the bf16 linear outputs and rounded once; the v block is stored as is.
+ * Replaces qkv Linear + q_norm/k_norm + rope of VGGT Attention.forward (ext
+ * layers/attention.py; aggregator frame/global blocks and the alignment
+ * head's frame blocks, alignment_head.py:351-366).  D in {64, 128},
+ * (H*D) % 128 == 0, K % 32 == 0.
+ */
+int vggt_gemm_qkv(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int M, int H, int D, int K,
+                  void* out, int64_t ldo, const float* qw, const float* qb, const float* kw, const float* kb, float eps,
+                  int rope_mode, const int32_t* pos, int period, const float* cos_tab, const float* sin_tab,
+                  int tab_len, void* stream);
+
+/*
  * Row LayerNorm over C (fp32 statistics): y = (x-mean)/sqrt(var+eps)*w + b.
  * w/b may be NULL (elementwise_affine=False).  Replaces nn.LayerNorm
  * (norm1/norm2 of every Block, alignment_head.py:203-206, DPT norm, ...).

@@ -28,6 +28,8 @@ _vp, _i, _i64, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_floa
 _SIGS = {
     "vggt_tune": [_i, _i],
     "vggt_gemm_bf16": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _vp, _i64, _vp, _vp, _i64, _vp],
+    "vggt_gemm_qkv": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _vp, _i64, _vp, _vp, _vp, _vp, _f, _i, _vp, _i, _vp,
+                      _vp, _i, _vp],
     "vggt_layernorm": [_vp, _i, _i64, _vp, _vp, _f, _i, _i, _vp, _i, _i64, _vp],
     "vggt_headnorm_rope": [_vp, _i64, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _i, _vp, _vp, _i, _vp],
     "vggt_attention_fwd": [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i, _i, _i, _i, _i, _f,
@@ -133,6 +135,21 @@ def gemm_bf16(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out: torch.T
     rc = lib().vggt_gemm_bf16(_p(a), _ld(a), _p(w), _ld(w), _p(bias), M, N, K, epi, _p(out), _ld(out), _p(gamma),
                               _p(out2), _ld(out2) if out2 is not None else 0, _stream())
     _check(rc, "vggt_gemm_bf16")
+    return out
+
+
+def gemm_qkv(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out: torch.Tensor, H: int, D: int, qw=None, qb=None,
+             kw=None, kb=None, eps: float = 0.0, mode: int = ROPE_NONE, pos=None, period: int = 1, cos=None,
+             sin=None) -> torch.Tensor:
+    """Fused qkv projection + q/k LayerNorm + RoPE (vggt_gemm_qkv)."""
+    _dev(a, "gemm_qkv")
+    M, K = a.shape
+    assert a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.shape == (3 * H * D, K)
+    assert out.shape[0] == M and out.shape[1] == 3 * H * D
+    tab = cos.shape[0] if cos is not None else 0
+    rc = lib().vggt_gemm_qkv(_p(a), _ld(a), _p(w), _ld(w), _p(bias), M, H, D, K, _p(out), _ld(out), _p(qw), _p(qb),
+                             _p(kw), _p(kb), float(eps), mode, _p(pos), period, _p(cos), _p(sin), tab, _stream())
+    _check(rc, "vggt_gemm_qkv")
     return out
 
 

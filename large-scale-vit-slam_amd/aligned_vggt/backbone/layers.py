@@ -127,11 +127,21 @@ class Block(nn.Module):
         N.layernorm(xs, self.norm1.weight, self.norm1.bias, self.norm1.eps, xn)
         w, b = pack_linear(self.attn.qkv)
         qkv = ws.buf("blk_qkv", M, 3 * C, torch.bfloat16)
-        N.gemm_bf16(xn, w, b, qkv, N.EPI_BF16)
         qn = self.attn.q_norm if isinstance(self.attn.q_norm, nn.LayerNorm) else None
         kn = self.attn.k_norm if isinstance(self.attn.k_norm, nn.LayerNorm) else None
         mode = rope.mode if (rope is not None and self.attn.rope is not None) else N.ROPE_NONE
-        if qn is not None or mode != N.ROPE_NONE:
+        fused = (qn is not None) == (kn is not None) and (qn is not None or mode != N.ROPE_NONE) and D in (64, 128) \
+            and (qn is None or qn.eps == kn.eps)
+        if fused:
+            # qkv projection with q_norm / k_norm + RoPE in the GEMM epilogue
+            rp = rope if mode != N.ROPE_NONE else None
+            N.gemm_qkv(xn, w, b, qkv, H, D, qn.weight if qn is not None else None, qn.bias if qn is not None else None,
+                       kn.weight if kn is not None else None, kn.bias if kn is not None else None,
+                       qn.eps if qn is not None else 0.0, mode, rp.pos if rp else None, rp.period if rp else 1,
+                       rp.cos if rp else None, rp.sin if rp else None)
+        else:
+            N.gemm_bf16(xn, w, b, qkv, N.EPI_BF16)
+        if not fused and (qn is not None or mode != N.ROPE_NONE):
             rp = rope if mode != N.ROPE_NONE else None
             N.qknorm_rope(qkv, H, D, qn.weight if qn is not None else None, qn.bias if qn is not None else None,
                           kn.weight if kn is not None else None, kn.bias if kn is not None else None,

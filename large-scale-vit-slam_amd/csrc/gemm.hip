@@ -35,7 +35,17 @@ struct Epi {
   const float* gamma;
   float* out2;
   int64_t ldo2;
+  // EPI_QKNORM (vggt_gemm_qkv): per-head LayerNorm of the q / k column blocks
+  // + RoPE, v block stored as is
+  const float *qw, *qb, *kw, *kb;
+  float eps;
+  int hd;  // H * D: width of each of the q / k / v column blocks
+  int rope_mode, period, tab_len;
+  const int32_t* pos;
+  const float *cs, *sn;
 };
+
+constexpr int EPI_QKNORM_D64 = 16, EPI_QKNORM_D128 = 17;  // internal epilogue ids
 
 // ---- epilogue 2 (shared): the bf16 C tile staged in LDS (row stride CROW
 // bytes) re-read as whole rows, 16 B (8 features) per thread, and written with
@@ -64,6 +74,70 @@ __device__ __forceinline__ void write_tile(const char* Cs, int m0, int n0, int M
     const uint4 cv = *(const uint4*)(Cs + ml * CROW + ch * 16);
     if constexpr (EPI == VGGT_EPI_BF16) {
       *(uint4*)((bf16_t*)ep.out + (int64_t)m * ep.ldo + n) = cv;
+    } else if constexpr (EPI == EPI_QKNORM_D64 || EPI == EPI_QKNORM_D128) {
+      // q / k blocks: q_norm / k_norm (fp32 LayerNorm over the head's D bf16
+      // linear outputs) then RoPE on the fp32 result, one bf16 rounding at the
+      // end -- the arithmetic of headnorm_rope_kernel (norm.hip), in registers.
+      constexpr int D = EPI == EPI_QKNORM_D64 ? 64 : 128;
+      constexpr int LPH = D / 8;  // lanes per head (consecutive: ch is the low index)
+      const int region = n0 / ep.hd;  // 0 q, 1 k, 2 v -- uniform per block
+      if (region >= 2) {
+        *(uint4*)((bf16_t*)ep.out + (int64_t)m * ep.ldo + n) = cv;
+        continue;
+      }
+      const uint32_t w4[4] = {cv.x, cv.y, cv.z, cv.w};
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x[2 * j] = bf2f((bf16_t)(w4[j] & 0xffff));
+        x[2 * j + 1] = bf2f((bf16_t)(w4[j] >> 16));
+      }
+      const int e0 = (n % ep.hd) % D;
+      const float* nw = region ? ep.kw : ep.qw;
+      const float* nb = region ? ep.kb : ep.qb;
+      if (nw) {
+        float sm = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sm += x[j];
+#pragma unroll
+        for (int o = 1; o < LPH; o <<= 1) sm += __shfl_xor(sm, o, 64);
+        const float mean = sm * (1.f / D);
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = x[j] - mean;
+          q += d * d;
+        }
+#pragma unroll
+        for (int o = 1; o < LPH; o <<= 1) q += __shfl_xor(q, o, 64);
+        const float rstd = rsqrtf(q * (1.f / D) + ep.eps);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = (x[j] - mean) * rstd * nw[e0 + j] + (nb ? nb[e0 + j] : 0.f);
+      }
+      if (ep.rope_mode != VGGT_ROPE_NONE) {
+        const bool two_d = ep.rope_mode == VGGT_ROPE_2D;
+        const int RD = two_d ? D / 2 : D;  // rotated block
+        const int PL = RD / 16;            // partner lane distance (rotate_half: RD/2 elements)
+        const int er = e0 % RD;
+        const int pr = m % ep.period;
+        int pp = two_d ? ep.pos[2 * pr + (e0 >= D / 2 ? 1 : 0)] : ep.pos[pr];
+        pp = min(max(pp, 0), ep.tab_len - 1);
+        const bool first = er < RD / 2;
+        float y[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float partner = __shfl_xor(x[j], PL, 64);
+          y[j] = x[j] * ep.cs[pp * RD + er + j] + (first ? -partner : partner) * ep.sn[pp * RD + er + j];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = y[j];
+      }
+      uint4 o;
+      o.x = pack_bf2(x[0], x[1]);
+      o.y = pack_bf2(x[2], x[3]);
+      o.z = pack_bf2(x[4], x[5]);
+      o.w = pack_bf2(x[6], x[7]);
+      *(uint4*)((bf16_t*)ep.out + (int64_t)m * ep.ldo + n) = o;
     } else {
       const uint32_t w4[4] = {cv.x, cv.y, cv.z, cv.w};
       float v[8];
@@ -449,6 +523,43 @@ extern "C" int vggt_gemm_bf16(const void* A, int64_t lda, const void* W, int64_t
     case VGGT_EPI_RESID_F32: gemm_bf16_kernel<VGGT_EPI_RESID_F32><<<nwg, NT, 0, s>>>(a, lda, w, ldw, M, N, K, ep); break;
     case VGGT_EPI_F32: gemm_bf16_kernel<VGGT_EPI_F32><<<nwg, NT, 0, s>>>(a, lda, w, ldw, M, N, K, ep); break;
     default: return VGGT_ERR_UNSUPPORTED;
+  }
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+extern "C" int vggt_gemm_qkv(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int M, int H,
+                             int D, int K, void* out, int64_t ldo, const float* qw, const float* qb, const float* kw,
+                             const float* kb, float eps, int rope_mode, const int32_t* pos, int period,
+                             const float* cos_tab, const float* sin_tab, int tab_len, void* stream) {
+  const int hd = H * D, N = 3 * hd;
+  if (M <= 0 || H <= 0 || K <= 0 || K % 32 || (D != 64 && D != 128) || hd % 128) return VGGT_ERR_SHAPE;
+  if ((qw == nullptr) != (kw == nullptr)) return VGGT_ERR_UNSUPPORTED;
+  if (rope_mode != VGGT_ROPE_NONE && rope_mode != VGGT_ROPE_2D && rope_mode != VGGT_ROPE_1D) return VGGT_ERR_UNSUPPORTED;
+  if (rope_mode != VGGT_ROPE_NONE && (!pos || !cos_tab || !sin_tab || period <= 0 || tab_len <= 0))
+    return VGGT_ERR_SHAPE;
+  if ((lda % 8) || (ldw % 8) || (ldo % 8) || ((uintptr_t)A & 15) || ((uintptr_t)W & 15) || ((uintptr_t)bias & 15) ||
+      ((uintptr_t)out & 15))
+    return VGGT_ERR_ALIGN;
+  Epi ep{bias, out, ldo, nullptr, nullptr, 0, qw, qb, kw, kb, eps, hd, rope_mode, period, tab_len, pos, cos_tab,
+         sin_tab};
+  hipStream_t s = (hipStream_t)stream;
+  const bf16_t* a = (const bf16_t*)A;
+  const bf16_t* w = (const bf16_t*)W;
+  int mode = g_vggt_gemm_tile < 0 ? 0 : g_vggt_gemm_tile;  // auto: the 128x128 form (measured faster for qkv)
+  if (mode == 0 && K % BK) mode = 2;
+  if (mode == 1 && hd % 256) mode = 2;
+  if (mode != 0 && (int64_t)RBM * (lda > ldw ? lda : ldw) * 2 >= (1ll << 31)) return VGGT_ERR_SHAPE;
+  if (mode == 0) {
+    const int nwg = ((M + BM - 1) / BM) * (N / BN);
+    if (D == 64) gemm_bf16_kernel<EPI_QKNORM_D64><<<nwg, NT, 0, s>>>(a, lda, w, ldw, M, N, K, ep);
+    else gemm_bf16_kernel<EPI_QKNORM_D128><<<nwg, NT, 0, s>>>(a, lda, w, ldw, M, N, K, ep);
+  } else if (mode == 1) {
+    if (D == 64) launch_ring<EPI_QKNORM_D64, 256>(a, lda, w, ldw, M, N, K, ep, s);
+    else launch_ring<EPI_QKNORM_D128, 256>(a, lda, w, ldw, M, N, K, ep, s);
+  } else {
+    if (D == 64) launch_ring<EPI_QKNORM_D64, 128>(a, lda, w, ldw, M, N, K, ep, s);
+    else launch_ring<EPI_QKNORM_D128, 128>(a, lda, w, ldw, M, N, K, ep, s);
   }
   HIP_LAUNCH_CHECK();
   return VGGT_OK;

@@ -239,3 +239,45 @@ def _online_softmax_rescale(N):
     t = qkv.float().view(1, n, 3, H, D).permute(2, 0, 3, 1, 4)
     ref = _ref_attn(t[0], t[1], t[2], D ** -0.5).permute(0, 2, 1, 3).reshape(n, C)
     assert _rel(o, ref) < 1e-2
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2])
+@pytest.mark.parametrize("D,H,mode,norm", [(64, 16, 1, True), (64, 16, 0, True), (128, 8, 1, True), (128, 8, 2, True),
+                                           (64, 4, 1, False)])
+def test_gemm_qkv_fused_matches_two_pass(N, tile, D, H, mode, norm):
+    """vggt_gemm_qkv (q/k LayerNorm + RoPE in the GEMM epilogue) against the
+    parity-tested two-launch path (gemm_bf16 + qknorm_rope)."""
+    from aligned_vggt.backbone.layers import RopeTables
+    M, C = 1500, H * D
+    K = 256
+    g = torch.Generator(device="cuda").manual_seed(D + H + mode)
+    a = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(3 * C, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
+    b = torch.randn(3 * C, device="cuda", generator=g).to(torch.bfloat16).float()
+    qw, qb, kw, kb = (torch.rand(D, device="cuda", generator=g) + 0.5 for _ in range(4))
+    if not norm:
+        qw = qb = kw = kb = None
+    if mode == 1:
+        yy, xx = torch.meshgrid(torch.arange(7), torch.arange(9), indexing="ij")
+        pos = torch.cat([torch.zeros(5, 2, dtype=torch.long), torch.stack([yy.reshape(-1), xx.reshape(-1)], -1) + 1])
+        rp = RopeTables(pos, D, 100.0, "cuda", N.ROPE_2D)
+    elif mode == 2:
+        rp = RopeTables(torch.arange(10), D, 100.0, "cuda", N.ROPE_1D)
+    else:
+        rp = None
+    args = (qw, qb, kw, kb, 1e-5 if norm else 0.0, mode, rp.pos if rp else None, rp.period if rp else 1,
+            rp.cos if rp else None, rp.sin if rp else None)
+    ref = torch.empty(M, 3 * C, device="cuda", dtype=torch.bfloat16)
+    N.gemm_bf16(a, w, b, ref, N.EPI_BF16)
+    N.qknorm_rope(ref, H, D, *args)
+    prev = N.tune(N.TUNE_GEMM_TILE, tile)
+    try:
+        out = torch.empty_like(ref)
+        N.gemm_qkv(a, w, b, out, H, D, *args)
+    finally:
+        N.tune(N.TUNE_GEMM_TILE, prev)
+    torch.cuda.synchronize()
+    d = (out.float() - ref.float()).abs()
+    # identical arithmetic up to fp32 contraction order: at most one bf16 ulp apart
+    assert (d <= ref.float().abs() * 2 ** -7 + 1e-6).all(), d.max().item()
+    assert torch.equal(out[:, 2 * C:], ref[:, 2 * C:])  # v block untouched
