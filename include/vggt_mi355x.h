@@ -219,6 +219,21 @@ int vggt_conv2d_f32(const float* x, int64_t ldx, int nimg, int hi, int wi, int c
                     const float* res1, int64_t ldr1, int res1_relu, const float* res2, int64_t ldr2, const float* pos,
                     int shuffle, void* stream);
 
+/*
+ * Same convolution as vggt_conv2d_f32 on the bf16 matrix path with split
+ * operands: x = hi + lo (hi = bf16(x), lo = bf16(x - hi)), accumulating
+ * hi.hi + hi.lo + lo.hi in fp32 (~2^-16 relative per product instead of
+ * fp32's 2^-24; ~5x faster).  w_hi / w_lo: the vggt_conv2d_f32 weight layout
+ * split by vggt_split_bf16x2 (bf16, rows padded to a multiple of 64).
+ */
+int vggt_conv2d_bf16x3(const float* x, int64_t ldx, int nimg, int hi, int wi, int ci, const void* w_hi,
+                       const void* w_lo, const float* bias, int co, int kh, int kw, int stride, int pad, float* y,
+                       int64_t ldy, int relu_in, int relu_out, const float* res1, int64_t ldr1, int res1_relu,
+                       const float* res2, int64_t ldr2, const float* pos, int shuffle, void* stream);
+
+/* hi[i] = bf16(x[i]), lo[i] = bf16(x[i] - hi[i]) for i < n (weight split for vggt_conv2d_bf16x3). */
+int vggt_split_bf16x2(const float* x, int64_t n, void* hi, void* lo, void* stream);
+
 /* NHWC bilinear resize with align_corners=True (custom_interpolate, dpt_head ext), + optional pos table. */
 int vggt_upsample_bilinear_f32(const float* x, int nimg, int hi, int wi, int C, float* y, int ho, int wo,
                                const float* pos, void* stream);

@@ -47,6 +47,9 @@ _SIGS = {
     "vggt_cast_f32_bf16": [_vp, _i64, _vp, _i64, _i, _i, _vp],
     "vggt_conv2d_f32": [_vp, _i64, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _i64, _i, _i, _vp, _i64, _i, _vp,
                         _i64, _vp, _i, _vp],
+    "vggt_conv2d_bf16x3": [_vp, _i64, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _i64, _i, _i, _vp, _i64,
+                           _i, _vp, _i64, _vp, _i, _vp],
+    "vggt_split_bf16x2": [_vp, _i64, _vp, _vp, _vp],
     "vggt_upsample_bilinear_f32": [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp],
     "vggt_dpt_activate": [_vp, _i64, _i64, _i, _i, _i, _vp, _vp, _vp, _vp],
     "vggt_irls_sim3": [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i, _i64, _f, _f, _i, _f, _vp, _vp, _vp, _vp,
@@ -298,6 +301,30 @@ def conv2d_f32(x: torch.Tensor, nimg: int, hi: int, wi: int, ci: int, w: torch.T
                                _stream())
     _check(rc, "vggt_conv2d_f32")
     return y
+
+
+def conv2d_bf16x3(x: torch.Tensor, nimg: int, hi: int, wi: int, ci: int, w_hi: torch.Tensor, w_lo: torch.Tensor, bias,
+                  co: int, kh: int, kw: int, stride: int, pad: int, y: torch.Tensor, relu_in: bool = False,
+                  relu_out: bool = False, res1: Optional[torch.Tensor] = None, res1_relu: bool = False,
+                  res2: Optional[torch.Tensor] = None, pos: Optional[torch.Tensor] = None, shuffle: int = 0):
+    """vggt_conv2d_f32 on the bf16 matrix path with split (hi + lo) operands."""
+    _dev(x, "conv2d_bf16x3")
+    rc = lib().vggt_conv2d_bf16x3(_p(x), _ld(x), nimg, hi, wi, ci, _p(w_hi), _p(w_lo), _p(bias), co, kh, kw, stride,
+                                  pad, _p(y), _ld(y), int(relu_in), int(relu_out), _p(res1),
+                                  _ld(res1) if res1 is not None else 0, int(res1_relu), _p(res2),
+                                  _ld(res2) if res2 is not None else 0, _p(pos), shuffle, _stream())
+    _check(rc, "vggt_conv2d_bf16x3")
+    return y
+
+
+def split_bf16x2(x: torch.Tensor):
+    """(hi, lo) bf16 tensors with x = hi + lo + O(2^-16 |x|)."""
+    _dev(x, "split_bf16x2")
+    x = x.contiguous().float()
+    hi = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    lo = torch.empty_like(hi)
+    _check(lib().vggt_split_bf16x2(_p(x), x.numel(), _p(hi), _p(lo), _stream()), "vggt_split_bf16x2")
+    return hi, lo
 
 
 def upsample_bilinear_f32(x: torch.Tensor, nimg: int, hi: int, wi: int, C: int, y: torch.Tensor, ho: int, wo: int,

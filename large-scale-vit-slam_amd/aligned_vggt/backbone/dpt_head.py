@@ -15,6 +15,8 @@ chunks 8 frames at a time only to bound memory -- the arithmetic is identical).
 """
 from __future__ import annotations
 
+import os
+
 from typing import List, Optional, Tuple
 
 import torch
@@ -91,14 +93,20 @@ def _scratch(in_shape, out_shape) -> nn.Module:
     return s
 
 
-def _pack_conv(conv: nn.Module, transpose: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+# DPT convolutions: "bf16x3" (split-bf16 operands on the bf16 matrix path,
+# ~2^-16 relative per product; default) or "fp32" (exact f32 MFMA).
+CONV_PRECISION = os.environ.get("VGGT_CONV", "bf16x3")
+
+
+def _pack_conv(conv: nn.Module, transpose: bool = False):
     """Conv2d [co,ci,kh,kw] -> [roundup(co,64), kh*kw*ci]; ConvTranspose2d
-    [ci,co,k,k] -> [roundup(k*k*co,64), ci] with column (ky*k+kx)*co + c."""
+    [ci,co,k,k] -> [roundup(k*k*co,64), ci] with column (ky*k+kx)*co + c.
+    Returns (w_f32, bias, w_hi, w_lo): the split bf16 halves are made once."""
     w = conv.weight
     key = (w.data_ptr(), w._version, transpose)
     c = conv.__dict__.get("_mi355x_conv")
     if c is not None and c[0] == key:
-        return c[1], c[2]
+        return c[1:]
     with torch.no_grad():
         if transpose:
             ci, co, kh, kw = w.shape
@@ -109,10 +117,23 @@ def _pack_conv(conv: nn.Module, transpose: bool = False) -> Tuple[torch.Tensor, 
         rows = (wp.shape[0] + 63) // 64 * 64
         if rows != wp.shape[0]:
             wp = torch.cat([wp, wp.new_zeros(rows - wp.shape[0], wp.shape[1])], 0)
+        wp = wp.contiguous()
         b = conv.bias.detach().float().contiguous() if conv.bias is not None else None
-        c = (key, wp.contiguous(), b)
+        w_hi, w_lo = N.split_bf16x2(wp) if wp.is_cuda else (None, None)
+        c = (key, wp, b, w_hi, w_lo)
     conv.__dict__["_mi355x_conv"] = c
-    return c[1], c[2]
+    return c[1:]
+
+
+def _conv_call(x_t, n, h, w_, c, packed, co, kh, kw, stride, pad, y, relu_in=False, relu_out=False, res1=None,
+               res1_relu=False, res2=None, pos=None, shuffle=0):
+    wp, b, w_hi, w_lo = packed
+    if CONV_PRECISION == "fp32":
+        N.conv2d_f32(x_t, n, h, w_, c, wp, b, co, kh, kw, stride, pad, y, relu_in, relu_out, res1, res1_relu, res2,
+                     pos, shuffle=shuffle)
+    else:
+        N.conv2d_bf16x3(x_t, n, h, w_, c, w_hi, w_lo, b, co, kh, kw, stride, pad, y, relu_in, relu_out, res1,
+                        res1_relu, res2, pos, shuffle=shuffle)
 
 
 class _Map:
@@ -126,23 +147,23 @@ class _Map:
 
 def _conv(x: _Map, conv: nn.Conv2d, stride=1, pad=None, relu_in=False, relu_out=False, res1: _Map = None,
           res1_relu=False, res2: _Map = None, pos=None) -> _Map:
-    wp, b = _pack_conv(conv)
+    packed = _pack_conv(conv)
     co, _, kh, kw = conv.weight.shape
     pad = conv.padding[0] if pad is None else pad
     ho = (x.h + 2 * pad - kh) // stride + 1
     wo = (x.w + 2 * pad - kw) // stride + 1
     y = torch.empty(x.n * ho * wo, co, device=x.t.device)
-    N.conv2d_f32(x.t, x.n, x.h, x.w, x.c, wp, b, co, kh, kw, stride, pad, y, relu_in, relu_out,
-                 res1.t if res1 else None, res1_relu, res2.t if res2 else None, pos)
+    _conv_call(x.t, x.n, x.h, x.w, x.c, packed, co, kh, kw, stride, pad, y, relu_in, relu_out,
+               res1.t if res1 else None, res1_relu, res2.t if res2 else None, pos)
     return _Map(y, x.n, ho, wo, co)
 
 
 def _convT(x: _Map, conv: nn.ConvTranspose2d) -> _Map:
-    wp, b = _pack_conv(conv, transpose=True)
+    packed = _pack_conv(conv, transpose=True)
     ci, co, k, _ = conv.weight.shape
     assert conv.stride[0] == k and conv.padding[0] == 0
     y = torch.empty(x.n * x.h * k * x.w * k, co, device=x.t.device)
-    N.conv2d_f32(x.t, x.n, x.h, x.w, x.c, wp, b, co, 1, 1, 1, 0, y, shuffle=k)
+    _conv_call(x.t, x.n, x.h, x.w, x.c, packed, co, 1, 1, 1, 0, y, shuffle=k)
     return _Map(y, x.n, x.h * k, x.w * k, co)
 
 

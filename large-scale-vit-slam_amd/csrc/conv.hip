@@ -2,8 +2,10 @@
 // vggt_upsample_bilinear_f32, vggt_dpt_activate).
 //
 // The reference runs the DPT heads with autocast disabled
-// (featureAligned_vggt.py:104), i.e. in fp32; so does this path: an implicit
-// GEMM over NHWC activations with exact-f32 MFMA (v_mfma_f32_16x16x4_f32).
+// (featureAligned_vggt.py:104), i.e. in fp32.  Two forms of one implicit GEMM
+// over NHWC activations: exact-f32 MFMA (v_mfma_f32_16x16x4_f32,
+// conv_f32_kernel) and split-bf16 (conv_bf16x3_kernel, below: fp32 operands
+// as bf16 hi + lo pairs on the bf16 matrix path, ~2^-16 per product).
 //   out[pixel, co] = sum_{ky,kx,ci} act(x[pixel@(ky,kx), ci]) * W[co, ky, kx, ci]
 // K is ordered (ky, kx, ci) with Ci % 32 == 0, so every 32-wide K slice is one
 // tap and a contiguous channel run (16-B loads, zero for padding taps).
@@ -34,6 +36,49 @@ struct ConvArgs {
   int shuffle;  // >0: ConvT pixel shuffle factor s; co is then the per-tap output channels
   int ncols;    // GEMM N (= co, or s*s*co for the shuffle)
 };
+
+// ---- shared epilogue: lane holds C[m = 4q + i][n = r16] of each 16x16 tile;
+// bias, ReLU, positional table, residual adds, pixel-shuffle store
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const f32x4 (&acc)[4][2], int M, int m0, int n0,
+                                              int wm, int wn, int r16, int q) {
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int n = n0 + wn * 32 + nt * 16 + r16;
+    if (n >= a.ncols) continue;
+    int co = n, dy = 0, dx = 0;
+    if (a.shuffle) {
+      const int tap = n / a.co;
+      co = n % a.co;
+      dy = tap / a.shuffle;
+      dx = tap % a.shuffle;
+    }
+    const float bv = a.bias ? a.bias[co] : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm * 64 + mt * 16 + 4 * q + i;
+        if (m >= M) continue;
+        float v = acc[mt][nt][i] + bv;
+        if (a.relu_out) v = fmaxf(v, 0.f);
+        int64_t opix;
+        if (a.shuffle) {
+          const int img = m / (a.ho * a.wo), rem = m % (a.ho * a.wo);
+          const int oy = (rem / a.wo) * a.shuffle + dy, ox = (rem % a.wo) * a.shuffle + dx;
+          opix = ((int64_t)img * a.ho * a.shuffle + oy) * (a.wo * a.shuffle) + ox;
+        } else {
+          opix = m;
+          if (a.pos) v += a.pos[(int64_t)(m % (a.ho * a.wo)) * a.co + co];
+          if (a.res1) {
+            const float r = a.res1[(int64_t)m * a.ldr1 + co];
+            v += a.res1_relu ? fmaxf(r, 0.f) : r;
+          }
+          if (a.res2) v += a.res2[(int64_t)m * a.ldr2 + co];
+        }
+        a.y[opix * a.ldy + co] = v;
+      }
+  }
+}
 
 __global__ __launch_bounds__(NT, 2) void conv_f32_kernel(ConvArgs a) {
   __shared__ __attribute__((aligned(16))) float As[2][BM * BK];
@@ -142,43 +187,152 @@ __global__ __launch_bounds__(NT, 2) void conv_f32_kernel(ConvArgs a) {
     __syncthreads();
   }
 
-  // ---- epilogue: lane holds C[m = 4q + i][n = r16] of each 16x16 tile ----
+  conv_epilogue(a, acc, M, m0, n0, wm, wn, r16, q);
+}
+
+
+// ===========================================================================
+// Split-bf16 ("bf16x3") form of the same implicit GEMM: every fp32 operand is
+// split as x = hi + lo with hi = bf16(x), lo = bf16(x - hi) (16 significant
+// bits), and the product is accumulated in fp32 as hi.hi + hi.lo + lo.hi on
+// v_mfma_f32_16x16x32_bf16 (the dropped lo.lo term and the split residue are
+// ~2^-16 relative).  Three bf16 MFMAs replace eight f32 ones per 32-deep K
+// slice, so the conv runs on the 2.5 PF bf16 matrix path instead of the
+// 157 TF f32 one.  Weights come pre-split (vggt_split_bf16x2); activations
+// are split on the fly after the (optional) input ReLU.
+// LDS: 64-B rows (32 bf16), swizzle chunk ^ h((row>>2)&3), h = {0,3,2,1}:
+// conflict-free ds_read_b128 fragment reads (as the GEMM ring).
+// ===========================================================================
+__device__ __forceinline__ int swz64(int row, int chunk) { return chunk ^ ((4 - ((row >> 2) & 3)) & 3); }
+
+__global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf16_t* __restrict__ whi,
+                                                            const bf16_t* __restrict__ wlo) {
+  constexpr int AT = BM * BK * 2, WT = BN * BK * 2;  // bytes of one bf16 A / W tile
+  constexpr int STG = 2 * AT + 2 * WT;               // Ahi, Alo, Whi, Wlo
+  __shared__ __attribute__((aligned(16))) char smem[2 * STG];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int M = a.nimg * a.ho * a.wo;
+  const int tiles_n = (a.ncols + BN - 1) / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (t / tiles_n) * BM;
+  const int n0 = (t % tiles_n) * BN;
+  const int K = a.kh * a.kw * a.ci;
+  const int nk = K / BK;
+
+  // A: rows r = tid/8 + 32*i, fp32 channel quad c4 = tid%8 (4 K values)
+  const int c4 = tid & 7;
+  int pn[4], py[4], px[4];
+  bool pv[4];
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    const int n = n0 + wn * 32 + nt * 16 + r16;
-    if (n >= a.ncols) continue;
-    int co = n, dy = 0, dx = 0;
-    if (a.shuffle) {
-      const int tap = n / a.co;
-      co = n % a.co;
-      dy = tap / a.shuffle;
-      dx = tap % a.shuffle;
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + (tid >> 3) + 32 * i;
+    pv[i] = m < M;
+    const int mm = pv[i] ? m : 0;
+    pn[i] = mm / (a.ho * a.wo);
+    const int rem = mm % (a.ho * a.wo);
+    py[i] = (rem / a.wo) * a.stride - a.pad;
+    px[i] = (rem % a.wo) * a.stride - a.pad;
+  }
+  // W: 64 rows x 32 K bf16 = 4 KiB per tile = 256 x 16 B: row tid/4, chunk tid%4
+  const int wr = tid >> 2, wch = tid & 3;
+  f32x4 ra[4];
+  uint4 rwh, rwl;
+
+  auto load = [&](int kt) {
+    const int k0 = kt * BK;
+    const int tap = k0 / a.ci;
+    const int ci0 = k0 % a.ci + c4 * 4;
+    const int ky = tap / a.kw, kx = tap % a.kw;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int iy = py[i] + ky, ix = px[i] + kx;
+      if (pv[i] && iy >= 0 && iy < a.hi && ix >= 0 && ix < a.wi) {
+        f32x4 v = *(const f32x4*)(a.x + (((int64_t)pn[i] * a.hi + iy) * a.wi + ix) * a.ldx + ci0);
+        if (a.relu_in) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+        }
+        ra[i] = v;
+      } else {
+        ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
-    const float bv = a.bias ? a.bias[co] : 0.f;
+    const int64_t wo = (int64_t)(n0 + wr) * K + k0 + wch * 8;  // weights padded to a multiple of BN rows
+    rwh = *(const uint4*)(whi + wo);
+    rwl = *(const uint4*)(wlo + wo);
+  };
+  auto store = [&](int buf) {
+    char* base = smem + buf * STG;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      uint2 h, l;
+      float hv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) hv[j] = round_bf(ra[i][j]);
+      h.x = pack_bf2(hv[0], hv[1]);
+      h.y = pack_bf2(hv[2], hv[3]);
+      l.x = pack_bf2(ra[i][0] - hv[0], ra[i][1] - hv[1]);
+      l.y = pack_bf2(ra[i][2] - hv[2], ra[i][3] - hv[3]);
+      const int off = r * 64 + (swz64(r, c4 >> 1) << 4) + (c4 & 1) * 8;
+      *(uint2*)(base + off) = h;
+      *(uint2*)(base + AT + off) = l;
+    }
+    const int woff = wr * 64 + (swz64(wr, wch) << 4);
+    *(uint4*)(base + 2 * AT + woff) = rwh;
+    *(uint4*)(base + 2 * AT + WT + woff) = rwl;
+  };
+
+  const int wm = wave >> 1, wn = wave & 1;
+  const int r16 = lane & 15, q = lane >> 4;
+  const int roff = r16 * 64 + (swz64(r16, q) << 4);  // fragment read offset (row & 15 == r16)
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load(kt + 1);
+    const char* base = smem + cur * STG;
+    bf16x8 ah[4], al[4], bh[2], bl[2];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int o = (wm * 64 + mt * 16) * 64 + roff;
+      ah[mt] = *(const bf16x8*)(base + o);
+      al[mt] = *(const bf16x8*)(base + AT + o);
+    }
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int o = (wn * 32 + nt * 16) * 64 + roff;
+      bh[nt] = *(const bf16x8*)(base + 2 * AT + o);
+      bl[nt] = *(const bf16x8*)(base + 2 * AT + WT + o);
+    }
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = m0 + wm * 64 + mt * 16 + 4 * q + i;
-        if (m >= M) continue;
-        float v = acc[mt][nt][i] + bv;
-        if (a.relu_out) v = fmaxf(v, 0.f);
-        int64_t opix;
-        if (a.shuffle) {
-          const int img = m / (a.ho * a.wo), rem = m % (a.ho * a.wo);
-          const int oy = (rem / a.wo) * a.shuffle + dy, ox = (rem % a.wo) * a.shuffle + dx;
-          opix = ((int64_t)img * a.ho * a.shuffle + oy) * (a.wo * a.shuffle) + ox;
-        } else {
-          opix = m;
-          if (a.pos) v += a.pos[(int64_t)(m % (a.ho * a.wo)) * a.co + co];
-          if (a.res1) {
-            const float r = a.res1[(int64_t)m * a.ldr1 + co];
-            v += a.res1_relu ? fmaxf(r, 0.f) : r;
-          }
-          if (a.res2) v += a.res2[(int64_t)m * a.ldr2 + co];
-        }
-        a.y[opix * a.ldy + co] = v;
+      for (int nt = 0; nt < 2; ++nt) {
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[mt], bh[nt], acc[mt][nt], 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mt], bl[nt], acc[mt][nt], 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mt], bh[nt], acc[mt][nt], 0, 0, 0);
       }
+    if (kt + 1 < nk) store(cur ^ 1);
+    __syncthreads();
+  }
+  conv_epilogue(a, acc, M, m0, n0, wm, wn, r16, q);
+}
+
+__global__ __launch_bounds__(256) void split_bf16x2_kernel(const float* __restrict__ x, int64_t n, bf16_t* __restrict__ hi,
+                                                           bf16_t* __restrict__ lo) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = x[i];
+    const float h = round_bf(v);
+    hi[i] = f2bf(h);
+    lo[i] = f2bf(v - h);
   }
 }
 
@@ -260,6 +414,54 @@ extern "C" int vggt_conv2d_f32(const float* x, int64_t ldx, int nimg, int hi, in
   const int64_t nwg = ((M + BM - 1) / BM) * ((a.ncols + BN - 1) / BN);
   if (nwg > 0x7fffffff) return VGGT_ERR_SHAPE;
   conv_f32_kernel<<<(int)nwg, NT, 0, (hipStream_t)stream>>>(a);
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+static int conv_args(ConvArgs& a, const float* x, int64_t ldx, int nimg, int hi, int wi, int ci, const float* w,
+                     const float* bias, int co, int kh, int kw, int stride, int pad, float* y, int64_t ldy, int relu_in,
+                     int relu_out, const float* res1, int64_t ldr1, int res1_relu, const float* res2, int64_t ldr2,
+                     const float* pos, int shuffle, int64_t* nwg) {
+  if (nimg <= 0 || hi <= 0 || wi <= 0 || ci <= 0 || co <= 0 || kh <= 0 || kw <= 0 || stride <= 0 || pad < 0)
+    return VGGT_ERR_SHAPE;
+  if (ci % BK) return VGGT_ERR_SHAPE;
+  if (shuffle && (kh != 1 || kw != 1 || stride != 1 || pad != 0 || res1 || res2 || pos)) return VGGT_ERR_UNSUPPORTED;
+  if ((ldx % 4) || ((uintptr_t)x % 16)) return VGGT_ERR_ALIGN;
+  a.x = x; a.w = w; a.bias = bias; a.y = y; a.res1 = res1; a.res2 = res2; a.pos = pos;
+  a.ldx = ldx; a.ldy = ldy; a.ldr1 = ldr1; a.ldr2 = ldr2;
+  a.nimg = nimg; a.hi = hi; a.wi = wi; a.ci = ci;
+  a.ho = (hi + 2 * pad - kh) / stride + 1;
+  a.wo = (wi + 2 * pad - kw) / stride + 1;
+  a.co = co; a.kh = kh; a.kw = kw; a.stride = stride; a.pad = pad;
+  a.relu_in = relu_in; a.relu_out = relu_out; a.res1_relu = res1_relu;
+  a.shuffle = shuffle;
+  a.ncols = shuffle ? shuffle * shuffle * co : co;
+  const int64_t M = (int64_t)nimg * a.ho * a.wo;
+  *nwg = ((M + BM - 1) / BM) * ((a.ncols + BN - 1) / BN);
+  if (*nwg > 0x7fffffff) return VGGT_ERR_SHAPE;
+  return VGGT_OK;
+}
+
+extern "C" int vggt_conv2d_bf16x3(const float* x, int64_t ldx, int nimg, int hi, int wi, int ci, const void* w_hi,
+                                  const void* w_lo, const float* bias, int co, int kh, int kw, int stride, int pad,
+                                  float* y, int64_t ldy, int relu_in, int relu_out, const float* res1, int64_t ldr1,
+                                  int res1_relu, const float* res2, int64_t ldr2, const float* pos, int shuffle,
+                                  void* stream) {
+  ConvArgs a;
+  int64_t nwg;
+  const int rc = conv_args(a, x, ldx, nimg, hi, wi, ci, nullptr, bias, co, kh, kw, stride, pad, y, ldy, relu_in,
+                           relu_out, res1, ldr1, res1_relu, res2, ldr2, pos, shuffle, &nwg);
+  if (rc) return rc;
+  if (((uintptr_t)w_hi % 16) || ((uintptr_t)w_lo % 16)) return VGGT_ERR_ALIGN;
+  conv_bf16x3_kernel<<<(int)nwg, NT, 0, (hipStream_t)stream>>>(a, (const bf16_t*)w_hi, (const bf16_t*)w_lo);
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+extern "C" int vggt_split_bf16x2(const float* x, int64_t n, void* hi, void* lo, void* stream) {
+  if (n < 0) return VGGT_ERR_SHAPE;
+  if (n == 0) return VGGT_OK;
+  split_bf16x2_kernel<<<grid_for(n), 256, 0, (hipStream_t)stream>>>(x, n, (bf16_t*)hi, (bf16_t*)lo);
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
 }

@@ -110,8 +110,18 @@ def test_layernorm_grouped_and_cast(N):
     assert torch.equal(xb, x.to(torch.bfloat16))
 
 
+def _conv_call(N, prec, xr, n, hi, wi, ci, wp, b, co, k, s, p, y, **kw):
+    if prec == "fp32":
+        return N.conv2d_f32(xr, n, hi, wi, ci, wp, b, co, k, k, s, p, y, **kw)
+    w_hi, w_lo = N.split_bf16x2(wp)
+    return N.conv2d_bf16x3(xr, n, hi, wi, ci, w_hi, w_lo, b, co, k, k, s, p, y, **kw)
+
+
+@pytest.mark.parametrize("prec,tol", [("fp32", 2e-6), ("bf16x3", 3e-5)])
 @pytest.mark.parametrize("case", ["3x3", "3x3s2", "1x1pos", "rcu", "shuffle4", "shuffle2", "co2"])
-def test_conv2d_f32(N, case):
+def test_conv2d_f32(N, case, prec, tol):
+    """fp32 implicit-GEMM conv (exact f32 MFMA) and its split-bf16 form
+    against torch fp32; the split form's tolerance is its 2^-16 operand split."""
     g = torch.Generator(device="cuda").manual_seed(hash(case) % 1000)
     n, hi, wi = 2, 13, 11
     ci, co, k, s, p = 64, 64, 3, 1, 1
@@ -131,9 +141,9 @@ def test_conv2d_f32(N, case):
         wp = torch.cat([wp, wp.new_zeros((-wp.shape[0]) % 64, ci)])
         xr = x.permute(0, 2, 3, 1).reshape(-1, ci).contiguous()
         y = torch.empty(n * hi * f * wi * f, co, device="cuda")
-        N.conv2d_f32(xr, n, hi, wi, ci, wp.contiguous(), bt, co, 1, 1, 1, 0, y, shuffle=f)
+        _conv_call(N, prec, xr, n, hi, wi, ci, wp.contiguous(), bt, co, 1, 1, 0, y, shuffle=f)
         got = y.view(n, hi * f, wi * f, co).permute(0, 3, 1, 2)
-        assert _rel(got, ref) < 2e-6
+        assert _rel(got, ref) < tol
         return
     x = torch.randn(n, ci, hi, wi, device="cuda", generator=g)
     w = torch.randn(co, ci, k, k, device="cuda", generator=g) / (ci * k * k) ** 0.5
@@ -155,7 +165,7 @@ def test_conv2d_f32(N, case):
     if case == "3x3":
         r1 = torch.randn(n * ho * wo, co, device="cuda", generator=g)
         r2 = torch.randn(n * ho * wo, co, device="cuda", generator=g)
-    N.conv2d_f32(xr, n, hi, wi, ci, wp, b, co, k, k, s, p, y, res1=r1, res1_relu=True, res2=r2, pos=pos, **kw)
+    _conv_call(N, prec, xr, n, hi, wi, ci, wp, b, co, k, s, p, y, res1=r1, res1_relu=True, res2=r2, pos=pos, **kw)
     ref = F.conv2d(ref_in, w, b, stride=s, padding=p)
     if case == "rcu":
         ref = F.relu(ref)
@@ -164,7 +174,7 @@ def test_conv2d_f32(N, case):
         ref = ref + pos.repeat(n, 1)
     if r1 is not None:
         ref = ref + F.relu(r1) + r2
-    assert _rel(y, ref) < 2e-6
+    assert _rel(y, ref) < tol
 
 
 def test_upsample_and_activate(N):
