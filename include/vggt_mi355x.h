@@ -182,6 +182,13 @@ int vggt_layernorm_grouped(const void* x, int in_dtype, int64_t ldx, const float
  */
 int vggt_linear_f32(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, int M, int N, int K,
                     int act_in, int epi, float* out, int64_t ldo, const float* gamma, void* stream);
+/* Same with a caller-provided scratch (device, >= 16 * roundup(M,64) * N floats
+ * to allow the maximum split): skinny-M calls are split along K into up to 16
+ * deterministic partial sums combined in a fixed order (camera head trunk,
+ * alignment decoder: M = 16 frames).  ws == NULL: no split. */
+int vggt_linear_f32_ws(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, int M, int N, int K,
+                       int act_in, int epi, float* out, int64_t ldo, const float* gamma, void* ws, size_t ws_bytes,
+                       void* stream);
 
 /*
  * Small-window attention (nk <= 128, D <= 256), one wave per (batch, head),

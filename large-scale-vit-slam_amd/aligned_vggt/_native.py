@@ -41,6 +41,7 @@ _SIGS = {
     "vggt_qknorm_rope": [_vp, _i64, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _i, _vp, _i, _vp, _vp, _i, _vp],
     "vggt_layernorm_grouped": [_vp, _i, _i64, _vp, _vp, _f, _i, _i, _vp, _i, _i64, _i, _i, _i, _i, _i, _vp],
     "vggt_linear_f32": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _i, _vp, _i64, _vp, _vp],
+    "vggt_linear_f32_ws": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _i, _vp, _i64, _vp, _vp, ctypes.c_size_t, _vp],
     "vggt_attention_small": [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i64, _i, _i, _i, _i, _i, _i, _f,
                              _vp],
     "vggt_headnorm_rope_f32": [_vp, _i64, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _i, _vp, _vp, _i, _vp],
@@ -255,10 +256,25 @@ def linear_f32(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], o
     M, K = a.shape
     N_ = w.shape[0]
     assert a.dtype == torch.float32 and w.dtype == torch.float32 and w.shape[1] == K and out.shape == (M, N_)
-    rc = lib().vggt_linear_f32(_p(a), _ld(a), _p(w), _ld(w), _p(bias), M, N_, K, act_in, epi, _p(out), _ld(out),
-                               _p(gamma), _stream())
-    _check(rc, "vggt_linear_f32")
+    # split-K scratch for skinny M (at most 16 splits of a 64-row-padded [M, N] fp32 slab)
+    need = 16 * ((M + 63) // 64) * 64 * N_
+    ws = _split_ws(a.device, need) if M <= 256 else None
+    rc = lib().vggt_linear_f32_ws(_p(a), _ld(a), _p(w), _ld(w), _p(bias), M, N_, K, act_in, epi, _p(out), _ld(out),
+                                  _p(gamma), _p(ws), 0 if ws is None else ws.numel() * 4, _stream())
+    _check(rc, "vggt_linear_f32_ws")
     return out
+
+
+_SPLIT_WS = {}
+
+
+def _split_ws(device, n_floats: int) -> torch.Tensor:
+    """Grow-only per-device scratch for split-K partial sums (stream-ordered reuse)."""
+    t = _SPLIT_WS.get(device)
+    if t is None or t.numel() < n_floats:
+        t = torch.empty(n_floats, device=device, dtype=torch.float32)
+        _SPLIT_WS[device] = t
+    return t
 
 
 def attention_small(q, k, v, o, batch: int, heads: int, nq: int, nk: int, D: int, q_bstride: int, k_bstride: int,

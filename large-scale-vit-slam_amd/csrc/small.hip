@@ -24,7 +24,13 @@ template <int ACT_IN, int EPI>
 __global__ __launch_bounds__(256) void linear_f32_kernel(const float* __restrict__ A, int64_t lda,
                                                          const float* __restrict__ W, int64_t ldw,
                                                          const float* __restrict__ bias, int M, int N, int K,
-                                                         float* out, int64_t ldo, const float* __restrict__ gamma) {
+                                                         float* out, int64_t ldo, const float* __restrict__ gamma,
+                                                         int kchunk, float* __restrict__ part) {
+  // split-K (part != NULL): block z covers K range [z*kchunk, (z+1)*kchunk) and
+  // stores its raw partial sums to part[z][M][N]; linear_f32_reduce applies
+  // bias and the epilogue.
+  const int kbeg = blockIdx.z * kchunk;
+  const int kend = min(K, kbeg + kchunk);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int n0 = (blockIdx.x * 4 + wave) * 16;
@@ -38,14 +44,14 @@ __global__ __launch_bounds__(256) void linear_f32_kernel(const float* __restrict
   const int mt_n = (M + 15) / 16;
   f32x4 acc[4] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
   const bool vec = ((K & 3) == 0) && ((lda & 3) == 0) && ((ldw & 3) == 0);
-  for (int k0 = 0; k0 < K; k0 += 16) {
+  for (int k0 = kbeg; k0 < kend; k0 += 16) {
     const int kk = k0 + 4 * q;
     f4 wv;
-    if (vec && kk + 3 < K) {
+    if (vec && kk + 3 < kend) {
       wv = *(const f4*)(W + (int64_t)nrow * ldw + kk);
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) wv[j] = (kk + j < K) ? W[(int64_t)nrow * ldw + kk + j] : 0.f;
+      for (int j = 0; j < 4; ++j) wv[j] = (kk + j < kend) ? W[(int64_t)nrow * ldw + kk + j] : 0.f;
     }
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
@@ -53,11 +59,11 @@ __global__ __launch_bounds__(256) void linear_f32_kernel(const float* __restrict
       const int m = mt * 16 + r;
       f4 av = f4{0, 0, 0, 0};
       if (m < M) {
-        if (vec && kk + 3 < K) {
+        if (vec && kk + 3 < kend) {
           av = *(const f4*)(A + (int64_t)m * lda + kk);
         } else {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) av[j] = (kk + j < K) ? A[(int64_t)m * lda + kk + j] : 0.f;
+          for (int j = 0; j < 4; ++j) av[j] = (kk + j < kend) ? A[(int64_t)m * lda + kk + j] : 0.f;
         }
         if constexpr (ACT_IN == 1) {  // SiLU on the input (poseLN_modulation = Sequential(SiLU, Linear))
 #pragma unroll
@@ -71,6 +77,19 @@ __global__ __launch_bounds__(256) void linear_f32_kernel(const float* __restrict
   // C[m = 16mt + 4q + i][n = n0 + r]
   const int n = n0 + r;
   if (n >= N) return;
+  if (part) {
+    float* pp = part + ((int64_t)blockIdx.z * gridDim.y * 64 + mbase) * N + n;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      if (mt >= mt_n) break;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = mt * 16 + 4 * q + i;
+        if (m < M) pp[(int64_t)m * N] = acc[mt][i];
+      }
+    }
+    return;
+  }
   const float bv = bias ? bias[n] : 0.f;
   const float g = (EPI == VGGT_EPI_RESID_F32) ? gamma[n] : 0.f;
 #pragma unroll
@@ -86,6 +105,24 @@ __global__ __launch_bounds__(256) void linear_f32_kernel(const float* __restrict
       if constexpr (EPI == VGGT_EPI_RESID_F32) v = *op + g * v;
       *op = v;
     }
+  }
+}
+
+// split-K combine: out = epi(sum_z part[z] + bias), fixed summation order
+template <int EPI>
+__global__ __launch_bounds__(256) void linear_f32_reduce(const float* __restrict__ part, int splits, int64_t mstride,
+                                                         int M, int N, const float* __restrict__ bias, float* out,
+                                                         int64_t ldo, const float* __restrict__ gamma) {
+  const int64_t total = (int64_t)M * N;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int m = (int)(e / N), n = (int)(e % N);
+    float v = 0.f;
+    for (int z = 0; z < splits; ++z) v += part[z * mstride + e];
+    v += bias ? bias[n] : 0.f;
+    float* op = out + (int64_t)m * ldo + n;
+    if constexpr (EPI == VGGT_EPI_GELU_BF16) v = gelu_erf(v);
+    if constexpr (EPI == VGGT_EPI_RESID_F32) v = *op + gamma[n] * v;
+    *op = v;
   }
 }
 
@@ -236,16 +273,26 @@ inline int grid_for(int64_t total) {
 
 }  // namespace
 
-extern "C" int vggt_linear_f32(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, int M,
-                               int N, int K, int act_in, int epi, float* out, int64_t ldo, const float* gamma,
-                               void* stream) {
+extern "C" int vggt_linear_f32_ws(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, int M,
+                                  int N, int K, int act_in, int epi, float* out, int64_t ldo, const float* gamma,
+                                  void* ws, size_t ws_bytes, void* stream) {
   if (M <= 0 || N <= 0 || K <= 0) return VGGT_ERR_SHAPE;
   if (epi == VGGT_EPI_RESID_F32 && !gamma) return VGGT_ERR_SHAPE;
   if ((act_in != 0 && act_in != 1) || (epi != VGGT_EPI_F32 && epi != VGGT_EPI_GELU_BF16 && epi != VGGT_EPI_RESID_F32))
     return VGGT_ERR_UNSUPPORTED;
-  const dim3 grid((N + 63) / 64, (M + 63) / 64);
+  const int gy = (M + 63) / 64;
+  const int blocks = ((N + 63) / 64) * gy;
+  // split K until ~2 blocks per CU are busy (skinny M: camera head, decoder)
+  int splits = 1;
+  while (splits < 16 && blocks * splits * 2 <= 512 && K / (splits * 2) >= 128) splits *= 2;
+  const int64_t mstride = (int64_t)gy * 64 * N;
+  if (splits > 1 && (!ws || ws_bytes < (size_t)splits * mstride * sizeof(float))) splits = 1;
+  const int kchunk = splits > 1 ? ((K + splits - 1) / splits + 15) / 16 * 16 : K;
+  float* part = splits > 1 ? (float*)ws : nullptr;
+  const dim3 grid((N + 63) / 64, gy, splits);
   hipStream_t s = (hipStream_t)stream;
-#define LAUNCH(AI, E) linear_f32_kernel<AI, E><<<grid, 256, 0, s>>>(A, lda, W, ldw, bias, M, N, K, out, ldo, gamma)
+#define LAUNCH(AI, E) \
+  linear_f32_kernel<AI, E><<<grid, 256, 0, s>>>(A, lda, W, ldw, bias, M, N, K, out, ldo, gamma, kchunk, part)
   if (act_in == 0) {
     if (epi == VGGT_EPI_F32) LAUNCH(0, VGGT_EPI_F32);
     else if (epi == VGGT_EPI_GELU_BF16) LAUNCH(0, VGGT_EPI_GELU_BF16);
@@ -256,8 +303,21 @@ extern "C" int vggt_linear_f32(const float* A, int64_t lda, const float* W, int6
     else LAUNCH(1, VGGT_EPI_RESID_F32);
   }
 #undef LAUNCH
+  if (part) {
+    const int64_t total = (int64_t)M * N;
+    const int rg = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+    if (epi == VGGT_EPI_F32) linear_f32_reduce<VGGT_EPI_F32><<<rg, 256, 0, s>>>(part, splits, mstride, M, N, bias, out, ldo, gamma);
+    else if (epi == VGGT_EPI_GELU_BF16) linear_f32_reduce<VGGT_EPI_GELU_BF16><<<rg, 256, 0, s>>>(part, splits, mstride, M, N, bias, out, ldo, gamma);
+    else linear_f32_reduce<VGGT_EPI_RESID_F32><<<rg, 256, 0, s>>>(part, splits, mstride, M, N, bias, out, ldo, gamma);
+  }
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
+}
+
+extern "C" int vggt_linear_f32(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, int M,
+                               int N, int K, int act_in, int epi, float* out, int64_t ldo, const float* gamma,
+                               void* stream) {
+  return vggt_linear_f32_ws(A, lda, W, ldw, bias, M, N, K, act_in, epi, out, ldo, gamma, nullptr, 0, stream);
 }
 
 extern "C" int vggt_attention_small(const void* q, int64_t ldq, int64_t q_bstride, const void* k, int64_t ldk,
