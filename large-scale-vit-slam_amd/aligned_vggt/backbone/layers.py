@@ -12,6 +12,8 @@ autocast semantics of the reference (featureAligned_vggt.py:78 under
 """
 from __future__ import annotations
 
+import os
+
 from typing import Optional, Tuple
 
 import torch
@@ -63,6 +65,11 @@ class Attention(nn.Module):
         self.proj = nn.Linear(dim, dim, bias=proj_bias)
         self.proj_drop = nn.Dropout(proj_drop)
         self.rope = rope
+
+
+# q/k norm + RoPE fused into the qkv GEMM epilogue (vggt_gemm_qkv); VGGT_FUSED_QKV=0
+# selects the separate headnorm_rope launch (A/B and fallback for odd shapes).
+_FUSED_QKV = os.environ.get("VGGT_FUSED_QKV", "1") != "0"
 
 
 class RopeTables:
@@ -130,8 +137,8 @@ class Block(nn.Module):
         qn = self.attn.q_norm if isinstance(self.attn.q_norm, nn.LayerNorm) else None
         kn = self.attn.k_norm if isinstance(self.attn.k_norm, nn.LayerNorm) else None
         mode = rope.mode if (rope is not None and self.attn.rope is not None) else N.ROPE_NONE
-        fused = (qn is not None) == (kn is not None) and (qn is not None or mode != N.ROPE_NONE) and D in (64, 128) \
-            and (qn is None or qn.eps == kn.eps)
+        fused = _FUSED_QKV and (qn is not None) == (kn is not None) and (qn is not None or mode != N.ROPE_NONE) \
+            and D in (64, 128) and (qn is None or qn.eps == kn.eps)
         if fused:
             # qkv projection with q_norm / k_norm + RoPE in the GEMM epilogue
             rp = rope if mode != N.ROPE_NONE else None

@@ -51,12 +51,32 @@ constexpr int EPI_QKNORM_D64 = 16, EPI_QKNORM_D128 = 17;  // internal epilogue i
 // bytes) re-read as whole rows, 16 B (8 features) per thread, and written with
 // coalesced stores, applying GELU / LayerScale + fp32 residual there.
 template <int EPI, int BM, int BN, int NT, int CROW>
-__device__ __forceinline__ void write_tile(const char* Cs, int m0, int n0, int M, const Epi& ep) {
+__device__ __forceinline__ void write_tile(const char* Cs, int m0, int n0, int M, const Epi& ep,
+                                           const float* tcs = nullptr, const float* tsn = nullptr) {
   constexpr int CPR = BN / 8;        // 16-B chunks per row
   constexpr int RPP = NT / CPR;      // rows per pass
   const int ch = threadIdx.x % CPR;
   const int n = n0 + ch * 8;
   float g[8];
+  // EPI_QKNORM: this thread's 8 norm weights / biases (fixed column), RoPE
+  // tables from LDS when the caller staged them there
+  float nwv[8], nbv[8];
+  if constexpr (EPI == EPI_QKNORM_D64 || EPI == EPI_QKNORM_D128) {
+    constexpr int D = EPI == EPI_QKNORM_D64 ? 64 : 128;
+    const int region = n0 / ep.hd;
+    const int e0 = (n % ep.hd) % D;
+    const float* nw = region ? ep.kw : ep.qw;
+    const float* nb = region ? ep.kb : ep.qb;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      nwv[j] = (region < 2 && nw) ? nw[e0 + j] : 1.f;
+      nbv[j] = (region < 2 && nb) ? nb[e0 + j] : 0.f;
+    }
+    if (!tcs) {
+      tcs = ep.cs;
+      tsn = ep.sn;
+    }
+  }
   if constexpr (EPI == VGGT_EPI_RESID_F32) {
     const f32x4 g0 = *(const f32x4*)(ep.gamma + n);
     const f32x4 g1 = *(const f32x4*)(ep.gamma + n + 4);
@@ -93,9 +113,7 @@ __device__ __forceinline__ void write_tile(const char* Cs, int m0, int n0, int M
         x[2 * j + 1] = bf2f((bf16_t)(w4[j] >> 16));
       }
       const int e0 = (n % ep.hd) % D;
-      const float* nw = region ? ep.kw : ep.qw;
-      const float* nb = region ? ep.kb : ep.qb;
-      if (nw) {
+      if (ep.qw) {
         float sm = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) sm += x[j];
@@ -112,7 +130,7 @@ __device__ __forceinline__ void write_tile(const char* Cs, int m0, int n0, int M
         for (int o = 1; o < LPH; o <<= 1) q += __shfl_xor(q, o, 64);
         const float rstd = rsqrtf(q * (1.f / D) + ep.eps);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) x[j] = (x[j] - mean) * rstd * nw[e0 + j] + (nb ? nb[e0 + j] : 0.f);
+        for (int j = 0; j < 8; ++j) x[j] = (x[j] - mean) * rstd * nwv[j] + nbv[j];
       }
       if (ep.rope_mode != VGGT_ROPE_NONE) {
         const bool two_d = ep.rope_mode == VGGT_ROPE_2D;
@@ -127,7 +145,7 @@ __device__ __forceinline__ void write_tile(const char* Cs, int m0, int n0, int M
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float partner = __shfl_xor(x[j], PL, 64);
-          y[j] = x[j] * ep.cs[pp * RD + er + j] + (first ? -partner : partner) * ep.sn[pp * RD + er + j];
+          y[j] = x[j] * tcs[pp * RD + er + j] + (first ? -partner : partner) * tsn[pp * RD + er + j];
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) x[j] = y[j];
@@ -262,6 +280,22 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(const bf16_t* __restri
   }
   __syncthreads();
 
+  if constexpr (EPI == EPI_QKNORM_D64 || EPI == EPI_QKNORM_D128) {
+    // RoPE cos/sin tables (a few KiB) into the LDS left over by the C tile
+    constexpr int D = EPI == EPI_QKNORM_D64 ? 64 : 128;
+    const int rd = ep.rope_mode == VGGT_ROPE_2D ? D / 2 : D;
+    const int tab = ep.rope_mode != VGGT_ROPE_NONE ? ep.tab_len * rd : 0;
+    float* ts = (float*)(smem + BM * CROW);
+    if (tab > 0 && n0 < 2 * ep.hd && 2 * tab * 4 <= (int)sizeof(smem) - BM * CROW) {
+      for (int i = threadIdx.x; i < tab; i += NT) {
+        ts[i] = ep.cs[i];
+        ts[tab + i] = ep.sn[i];
+      }
+      __syncthreads();
+      write_tile<EPI, BM, BN, NT, CROW>(Cs, m0, n0, M, ep, ts, ts + tab);
+      return;
+    }
+  }
   write_tile<EPI, BM, BN, NT, CROW>(Cs, m0, n0, M, ep);
 }
 
