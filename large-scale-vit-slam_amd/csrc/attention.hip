@@ -103,7 +103,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
   constexpr int RPI = 1024 / ROWB;       // rows per 1-KiB DMA instruction
   constexpr int CPR = ROWB / 16;         // 16-B chunks per row
   constexpr int IPW = TILEB / 1024 / NW;  // DMA instructions per wave per operand
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILEB];
+  constexpr int NSLOT = (VAR & 16) ? 3 : 2;  // K|V tile slots (3: pipelined QK^T)
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * 2 * TILEB];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -186,10 +187,13 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
   const float c = a.c;
   const int nt = (a.nk + BKV - 1) / BKV;
 
-  auto tile = [&](auto bufc, int t) {
+  struct S2 {
+    f32x16 v[2];
+  };
+  // ---- S^T = K . Q^T for the two 32-key blocks of the tile in slot BUF
+  auto qk = [&](auto bufc) -> S2 {
     constexpr int BUF = decltype(bufc)::value;
     const char* base = smem + BUF * 2 * TILEB;
-    // ---- S^T = K . Q^T for two 32-key blocks
     f32x16 s[2];
     if constexpr (VAR & 1) {
       // all K fragment reads first, then the two 32-key accumulator chains
@@ -217,6 +221,13 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
         }
       }
     }
+    return S2{{s[0], s[1]}};
+  };
+  // ---- mask, online softmax and O^T += V^T . P^T for the tile in slot BUF
+  auto soft_pv = [&](auto bufc, int t, S2 sc) {
+    constexpr int BUF = decltype(bufc)::value;
+    const char* base = smem + BUF * 2 * TILEB;
+    f32x16 s[2] = {sc.v[0], sc.v[1]};
     const int kv0 = t * BKV;
     if (kv0 + BKV > a.nk) {
 #pragma unroll
@@ -302,19 +313,54 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
     }
   };
 
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int t = 0; t < nt; t += 2) {
-    if (t + 1 < nt) stage(1, t + 1);
-    tile(std::integral_constant<int, 0>{}, t);
+  auto tile = [&](auto bufc, int t) { soft_pv(bufc, t, qk(bufc)); };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+
+  if constexpr (VAR & 16) {
+    // Pipelined: the QK^T MFMAs of tile t+1 are issued before tile t's softmax
+    // (T15), so the matrix pipe works while the VALU does exp / max / cvt.
+    // 3 slots: t (V read by P.V), t+1 (K read by QK^T), t+2 (DMA in flight,
+    // issued after the barrier that retires slot t-1).
+    stage(0, 0);
+    if (nt > 1) stage(1, 1);
+    if (nt > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * IPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    S2 cur = qk(I0{});
+    auto step = [&](auto sc, auto sn, auto sf, int t) {
+      // tile t+1 landed everywhere; every wave done with slot (t-1)%3 = (t+2)%3
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t + 2 < nt) stage(decltype(sf)::value, t + 2);
+      S2 nxt = cur;
+      if (t + 1 < nt) nxt = qk(sn);
+      soft_pv(sc, t, cur);
+      cur = nxt;
+    };
+    for (int t = 0; t < nt; t += 3) {
+      step(I0{}, I1{}, I2{}, t);
+      if (t + 1 >= nt) break;
+      step(I1{}, I2{}, I0{}, t + 1);
+      if (t + 2 >= nt) break;
+      step(I2{}, I0{}, I1{}, t + 2);
+    }
+  } else {
+    stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (t + 1 >= nt) break;
-    if (t + 2 < nt) stage(0, t + 2);
-    tile(std::integral_constant<int, 1>{}, t + 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    for (int t = 0; t < nt; t += 2) {
+      if (t + 1 < nt) stage(1, t + 1);
+      tile(I0{}, t);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t + 1 >= nt) break;
+      if (t + 2 < nt) stage(0, t + 2);
+      tile(I1{}, t + 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: normalise, O[q][d] bf16
@@ -360,6 +406,13 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
   const int nw = (g_vggt_attn_waves == 8 && nq >= 4096) ? 8 : 4;
   const int nwg = ((nq + nw * 32 - 1) / (nw * 32)) * heads * batch;
   hipStream_t s = (hipStream_t)stream;
+  if ((g_vggt_attn_variant == 19 || g_vggt_attn_variant == 23) && D == 64) {  // pipelined QK^T (3 LDS slots)
+    if (nw == 8) attn_fwd_kernel<64, 8, 19><<<nwg, 512, 0, s>>>(a);
+    else if (g_vggt_attn_variant == 23) attn_fwd_kernel<64, 4, 23><<<nwg, 256, 0, s>>>(a);
+    else attn_fwd_kernel<64, 4, 19><<<nwg, 256, 0, s>>>(a);
+    HIP_LAUNCH_CHECK();
+    return VGGT_OK;
+  }
   switch ((D == 64 ? 0 : 32) + (nw == 8 ? 16 : 0) + (g_vggt_attn_variant & 15)) {
 #define VGGT_ATTN_CASE(DD, NWW, V) \
   case (DD == 64 ? 0 : 32) + (NWW == 8 ? 16 : 0) + V: attn_fwd_kernel<DD, NWW, V><<<nwg, NWW * 64, 0, s>>>(a); break;

@@ -32,7 +32,7 @@ extern "C" int vggt_tune(int knob, int value) {
       g_vggt_attn_waves = value;
       return prev;
     case VGGT_TUNE_ATTN_VARIANT:
-      if (value < 0 || value > 15) return VGGT_ERR_UNSUPPORTED;
+      if (value < 0 || (value > 15 && value != 19 && value != 23)) return VGGT_ERR_UNSUPPORTED;
       prev = g_vggt_attn_variant;
       g_vggt_attn_variant = value;
       return prev;

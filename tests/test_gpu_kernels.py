@@ -157,7 +157,7 @@ def _ref_attn(q, k, v, scale):
     return torch.softmax(s, -1) @ v.float()
 
 
-@pytest.mark.parametrize("variant", [3, 11, 15])
+@pytest.mark.parametrize("variant", [3, 11, 15, 19, 23])
 @pytest.mark.parametrize("D,H,batch,n", [(64, 16, 3, 21), (64, 16, 2, 1374), (128, 8, 2, 1375), (64, 2, 1, 4100),
                                          (128, 2, 1, 64), (64, 1, 1, 1)])
 def test_attention_vs_torch(N, D, H, batch, n, variant):
@@ -214,7 +214,7 @@ def test_attention_global_shape_rows(N):
     assert _rel(o[rows], ref) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [3, 11])
+@pytest.mark.parametrize("variant", [3, 11, 19])
 def test_attention_online_softmax_rescale(N, variant):
     """Force the running max to jump late (rule 26): one key with a huge score
     in the last tile for some rows."""
