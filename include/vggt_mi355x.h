@@ -231,7 +231,7 @@ int vggt_conv2d_f32(const float* x, int64_t ldx, int nimg, int hi, int wi, int c
  * operands: x = hi + lo (hi = bf16(x), lo = bf16(x - hi)), accumulating
  * hi.hi + hi.lo + lo.hi in fp32 (~2^-16 relative per product instead of
  * fp32's 2^-24; ~5x faster).  w_hi / w_lo: the vggt_conv2d_f32 weight layout
- * split by vggt_split_bf16x2 (bf16, rows padded to a multiple of 64).
+ * split by vggt_split_bf16x2 (bf16), rows zero-padded to a multiple of 128.
  */
 int vggt_conv2d_bf16x3(const float* x, int64_t ldx, int nimg, int hi, int wi, int ci, const void* w_hi,
                        const void* w_lo, const float* bias, int co, int kh, int kw, int stride, int pad, float* y,

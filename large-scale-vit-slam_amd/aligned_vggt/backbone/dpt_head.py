@@ -99,8 +99,8 @@ CONV_PRECISION = os.environ.get("VGGT_CONV", "bf16x3")
 
 
 def _pack_conv(conv: nn.Module, transpose: bool = False):
-    """Conv2d [co,ci,kh,kw] -> [roundup(co,64), kh*kw*ci]; ConvTranspose2d
-    [ci,co,k,k] -> [roundup(k*k*co,64), ci] with column (ky*k+kx)*co + c.
+    """Conv2d [co,ci,kh,kw] -> [roundup(co,128), kh*kw*ci]; ConvTranspose2d
+    [ci,co,k,k] -> [roundup(k*k*co,128), ci] with column (ky*k+kx)*co + c.
     Returns (w_f32, bias, w_hi, w_lo): the split bf16 halves are made once."""
     w = conv.weight
     key = (w.data_ptr(), w._version, transpose)
@@ -114,7 +114,7 @@ def _pack_conv(conv: nn.Module, transpose: bool = False):
         else:
             co, ci, kh, kw = w.shape
             wp = w.detach().float().permute(0, 2, 3, 1).reshape(co, kh * kw * ci)
-        rows = (wp.shape[0] + 63) // 64 * 64
+        rows = (wp.shape[0] + 127) // 128 * 128  # (the f32 kernel needs 64, the split one 128)
         if rows != wp.shape[0]:
             wp = torch.cat([wp, wp.new_zeros(rows - wp.shape[0], wp.shape[1])], 0)
         wp = wp.contiguous()

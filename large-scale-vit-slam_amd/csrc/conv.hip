@@ -39,11 +39,12 @@ struct ConvArgs {
 
 // ---- shared epilogue: lane holds C[m = 4q + i][n = r16] of each 16x16 tile;
 // bias, ReLU, positional table, residual adds, pixel-shuffle store
-__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const f32x4 (&acc)[4][2], int M, int m0, int n0,
+template <int NTN>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const f32x4 (&acc)[4][NTN], int M, int m0, int n0,
                                               int wm, int wn, int r16, int q) {
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    const int n = n0 + wn * 32 + nt * 16 + r16;
+  for (int nt = 0; nt < NTN; ++nt) {
+    const int n = n0 + wn * NTN * 16 + nt * 16 + r16;
     if (n >= a.ncols) continue;
     int co = n, dy = 0, dx = 0;
     if (a.shuffle) {
@@ -205,19 +206,22 @@ __global__ __launch_bounds__(NT, 2) void conv_f32_kernel(ConvArgs a) {
 // ===========================================================================
 __device__ __forceinline__ int swz64(int row, int chunk) { return chunk ^ ((4 - ((row >> 2) & 3)) & 3); }
 
+template <int BNX>
 __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf16_t* __restrict__ whi,
                                                             const bf16_t* __restrict__ wlo) {
-  constexpr int AT = BM * BK * 2, WT = BN * BK * 2;  // bytes of one bf16 A / W tile
+  constexpr int NTN = BNX / 32;                       // 16-col fragments per wave (2 waves along N)
+  constexpr int WLD = BNX / 64;                       // 16-B W loads per thread per half
+  constexpr int AT = BM * BK * 2, WT = BNX * BK * 2;  // bytes of one bf16 A / W tile
   constexpr int STG = 2 * AT + 2 * WT;               // Ahi, Alo, Whi, Wlo
   __shared__ __attribute__((aligned(16))) char smem[2 * STG];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int M = a.nimg * a.ho * a.wo;
-  const int tiles_n = (a.ncols + BN - 1) / BN;
+  const int tiles_n = (a.ncols + BNX - 1) / BNX;
   const int tiles_m = (M + BM - 1) / BM;
   const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
   const int m0 = (t / tiles_n) * BM;
-  const int n0 = (t % tiles_n) * BN;
+  const int n0 = (t % tiles_n) * BNX;
   const int K = a.kh * a.kw * a.ci;
   const int nk = K / BK;
 
@@ -235,10 +239,10 @@ __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf
     py[i] = (rem / a.wo) * a.stride - a.pad;
     px[i] = (rem % a.wo) * a.stride - a.pad;
   }
-  // W: 64 rows x 32 K bf16 = 4 KiB per tile = 256 x 16 B: row tid/4, chunk tid%4
+  // W: BNX rows x 32 K bf16 = BNX*64 B per half: row tid/4 + 64*i, chunk tid%4
   const int wr = tid >> 2, wch = tid & 3;
   f32x4 ra[4];
-  uint4 rwh, rwl;
+  uint4 rwh[WLD], rwl[WLD];
 
   auto load = [&](int kt) {
     const int k0 = kt * BK;
@@ -259,9 +263,12 @@ __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf
         ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
-    const int64_t wo = (int64_t)(n0 + wr) * K + k0 + wch * 8;  // weights padded to a multiple of BN rows
-    rwh = *(const uint4*)(whi + wo);
-    rwl = *(const uint4*)(wlo + wo);
+#pragma unroll
+    for (int i = 0; i < WLD; ++i) {
+      const int64_t wo = (int64_t)(n0 + wr + 64 * i) * K + k0 + wch * 8;  // weights padded to a multiple of 128 rows
+      rwh[i] = *(const uint4*)(whi + wo);
+      rwl[i] = *(const uint4*)(wlo + wo);
+    }
   };
   auto store = [&](int buf) {
     char* base = smem + buf * STG;
@@ -280,17 +287,23 @@ __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf
       *(uint2*)(base + off) = h;
       *(uint2*)(base + AT + off) = l;
     }
-    const int woff = wr * 64 + (swz64(wr, wch) << 4);
-    *(uint4*)(base + 2 * AT + woff) = rwh;
-    *(uint4*)(base + 2 * AT + WT + woff) = rwl;
+#pragma unroll
+    for (int i = 0; i < WLD; ++i) {
+      const int rr = wr + 64 * i;
+      const int woff = rr * 64 + (swz64(rr, wch) << 4);
+      *(uint4*)(base + 2 * AT + woff) = rwh[i];
+      *(uint4*)(base + 2 * AT + WT + woff) = rwl[i];
+    }
   };
 
   const int wm = wave >> 1, wn = wave & 1;
   const int r16 = lane & 15, q = lane >> 4;
   const int roff = r16 * 64 + (swz64(r16, q) << 4);  // fragment read offset (row & 15 == r16)
-  f32x4 acc[4][2];
+  f32x4 acc[4][NTN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NTN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   load(0);
   store(0);
@@ -299,7 +312,7 @@ __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf
     const int cur = kt & 1;
     if (kt + 1 < nk) load(kt + 1);
     const char* base = smem + cur * STG;
-    bf16x8 ah[4], al[4], bh[2], bl[2];
+    bf16x8 ah[4], al[4], bh[NTN], bl[NTN];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       const int o = (wm * 64 + mt * 16) * 64 + roff;
@@ -307,15 +320,15 @@ __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf
       al[mt] = *(const bf16x8*)(base + AT + o);
     }
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const int o = (wn * 32 + nt * 16) * 64 + roff;
+    for (int nt = 0; nt < NTN; ++nt) {
+      const int o = (wn * NTN * 16 + nt * 16) * 64 + roff;
       bh[nt] = *(const bf16x8*)(base + 2 * AT + o);
       bl[nt] = *(const bf16x8*)(base + 2 * AT + WT + o);
     }
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
+      for (int nt = 0; nt < NTN; ++nt) {
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[mt], bh[nt], acc[mt][nt], 0, 0, 0);
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mt], bl[nt], acc[mt][nt], 0, 0, 0);
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mt], bh[nt], acc[mt][nt], 0, 0, 0);
@@ -323,7 +336,7 @@ __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf
     if (kt + 1 < nk) store(cur ^ 1);
     __syncthreads();
   }
-  conv_epilogue(a, acc, M, m0, n0, wm, wn, r16, q);
+  conv_epilogue<NTN>(a, acc, M, m0, n0, wm, wn, r16, q);
 }
 
 __global__ __launch_bounds__(256) void split_bf16x2_kernel(const float* __restrict__ x, int64_t n, bf16_t* __restrict__ hi,
@@ -453,7 +466,14 @@ extern "C" int vggt_conv2d_bf16x3(const float* x, int64_t ldx, int nimg, int hi,
                            relu_out, res1, ldr1, res1_relu, res2, ldr2, pos, shuffle, &nwg);
   if (rc) return rc;
   if (((uintptr_t)w_hi % 16) || ((uintptr_t)w_lo % 16)) return VGGT_ERR_ALIGN;
-  conv_bf16x3_kernel<<<(int)nwg, NT, 0, (hipStream_t)stream>>>(a, (const bf16_t*)w_hi, (const bf16_t*)w_lo);
+  // 128-wide N tiles when there are at least 128 GEMM columns (more MFMA work
+  // per split of the activation tile), else 64
+  if (a.ncols >= 128) {
+    const int64_t nw2 = (nwg / ((a.ncols + BN - 1) / BN)) * ((a.ncols + 127) / 128);
+    conv_bf16x3_kernel<128><<<(int)nw2, NT, 0, (hipStream_t)stream>>>(a, (const bf16_t*)w_hi, (const bf16_t*)w_lo);
+  } else {
+    conv_bf16x3_kernel<64><<<(int)nwg, NT, 0, (hipStream_t)stream>>>(a, (const bf16_t*)w_hi, (const bf16_t*)w_lo);
+  }
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
 }

@@ -119,7 +119,7 @@ def _conv_call(N, prec, xr, n, hi, wi, ci, wp, b, co, k, s, p, y, **kw):
 
 
 @pytest.mark.parametrize("prec,tol", [("fp32", 2e-6), ("bf16x3", 3e-5)])
-@pytest.mark.parametrize("case", ["3x3", "3x3s2", "1x1pos", "rcu", "shuffle4", "shuffle2", "co2"])
+@pytest.mark.parametrize("case", ["3x3", "3x3s2", "1x1pos", "rcu", "shuffle4", "shuffle2", "co2", "co256", "co192"])
 def test_conv2d_f32(N, case, prec, tol):
     """fp32 implicit-GEMM conv (exact f32 MFMA) and its split-bf16 form
     against torch fp32; the split form's tolerance is its 2^-16 operand split."""
@@ -132,6 +132,10 @@ def test_conv2d_f32(N, case, prec, tol):
         k, p, co = 1, 0, 128
     if case == "co2":
         k, p, ci, co = 1, 0, 32, 2
+    if case == "co256":
+        co = 256
+    if case == "co192":  # partial 128-wide N tile
+        co, k, p = 192, 1, 0
     if case.startswith("shuffle"):
         f = int(case[-1])
         x = torch.randn(n, ci, hi, wi, device="cuda", generator=g)
@@ -139,7 +143,7 @@ def test_conv2d_f32(N, case, prec, tol):
         bt = torch.randn(co, device="cuda", generator=g)
         ref = F.conv_transpose2d(x, wt, bt, stride=f)
         wp = wt.permute(2, 3, 1, 0).reshape(f * f * co, ci)
-        wp = torch.cat([wp, wp.new_zeros((-wp.shape[0]) % 64, ci)])
+        wp = torch.cat([wp, wp.new_zeros((-wp.shape[0]) % 128, ci)])
         xr = x.permute(0, 2, 3, 1).reshape(-1, ci).contiguous()
         y = torch.empty(n * hi * f * wi * f, co, device="cuda")
         _conv_call(N, prec, xr, n, hi, wi, ci, wp.contiguous(), bt, co, 1, 1, 0, y, shuffle=f)
@@ -152,7 +156,7 @@ def test_conv2d_f32(N, case, prec, tol):
     ho, wo = (hi + 2 * p - k) // s + 1, (wi + 2 * p - k) // s + 1
     xr = x.permute(0, 2, 3, 1).reshape(-1, ci).contiguous()
     wp = w.permute(0, 2, 3, 1).reshape(co, -1)
-    wp = torch.cat([wp, wp.new_zeros((-co) % 64, wp.shape[1])]).contiguous()
+    wp = torch.cat([wp, wp.new_zeros((-co) % 128, wp.shape[1])]).contiguous()
     y = torch.empty(n * ho * wo, co, device="cuda")
     kw = {}
     ref_in = x
