@@ -50,6 +50,32 @@ __device__ __forceinline__ float gelu_fast(float x) {
   return x * (x >= 0.f ? fmaf(-0.5f, e, 1.0f) : 0.5f * e);
 }
 
+// Two GELUs at once: the polynomial, the final products and the select run as
+// packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: two lanes of work per
+// instruction); only rcp and exp2 stay scalar.  Same formula and error as
+// gelu_fast.  For pure-VALU epilogues (no MFMA in flight on the wave).
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+__device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
+  const f32x2 z = f32x2{fabsf(x[0]), fabsf(x[1])} * 0.70710678118654752440f;
+  const f32x2 d = z * 0.5f + 1.0f;
+  const f32x2 t = f32x2{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+  f32x2 p = f32x2{0.17087277f, 0.17087277f};
+  p = p * t + -0.82215223f;
+  p = p * t + 1.48851587f;
+  p = p * t + -1.13520398f;
+  p = p * t + 0.27886807f;
+  p = p * t + -0.18628806f;
+  p = p * t + 0.09678418f;
+  p = p * t + 0.37409196f;
+  p = p * t + 1.00002368f;
+  p = p * t + -1.26551223f;
+  const f32x2 arg = (p - z * z) * 1.4426950408889634f;
+  const f32x2 e = t * f32x2{__builtin_amdgcn_exp2f(arg[0]), __builtin_amdgcn_exp2f(arg[1])};  // erfc(z)
+  const f32x2 h = e * 0.5f;
+  const f32x2 phi = f32x2{x[0] >= 0.f ? 1.0f - h[0] : h[0], x[1] >= 0.f ? 1.0f - h[1] : h[1]};
+  return x * phi;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -166,10 +166,12 @@ __device__ __forceinline__ void write_tile(const char* Cs, int m0, int n0, int M
       }
       if constexpr (EPI == VGGT_EPI_GELU_BF16) {
         uint4 o;
-        o.x = pack_bf2(gelu_fast(v[0]), gelu_fast(v[1]));
-        o.y = pack_bf2(gelu_fast(v[2]), gelu_fast(v[3]));
-        o.z = pack_bf2(gelu_fast(v[4]), gelu_fast(v[5]));
-        o.w = pack_bf2(gelu_fast(v[6]), gelu_fast(v[7]));
+        const f32x2 g0 = gelu_fast2(f32x2{v[0], v[1]}), g1 = gelu_fast2(f32x2{v[2], v[3]});
+        const f32x2 g2 = gelu_fast2(f32x2{v[4], v[5]}), g3 = gelu_fast2(f32x2{v[6], v[7]});
+        o.x = pack_bf2(g0[0], g0[1]);
+        o.y = pack_bf2(g1[0], g1[1]);
+        o.z = pack_bf2(g2[0], g2[1]);
+        o.w = pack_bf2(g3[0], g3[1]);
         *(uint4*)((bf16_t*)ep.out + (int64_t)m * ep.ldo + n) = o;
       } else if constexpr (EPI == VGGT_EPI_RESID_F32) {
         float* xp = (float*)ep.out + (int64_t)m * ep.ldo + n;

@@ -194,3 +194,27 @@ def test_sequence_ate_rpe_parity(models):
     for k in m_ref:
         spread = abs(m_32[k] - m_ref[k])
         assert abs(m_hip[k] - m_ref[k]) <= max(5e-2 * abs(m_ref[k]), 1.5 * spread) + 1e-6, (k, m_hip, m_ref, m_32)
+
+
+def test_feature_aligned_batch2(models):
+    """B = 2 (two independent sequences in one call): every stage keeps the
+    batch elements apart (global attention per batch element, per-batch Sim(3)
+    composition); each element must equal its own B = 1 run."""
+    m, sd = models
+    from aligned_vggt.utils.synthetic import synthetic_images
+    S, ov, H, W = 3, 1, 42, 56
+    a = synthetic_images(1, 2 * S - ov, H, W, seed=21)
+    b = synthetic_images(1, 2 * S - ov, H, W, seed=22)
+    both = torch.cat([a, b], 0)
+    chunks = O.generate_chunks(both.shape[1], S, ov)
+    ctx2 = ctxa = ctxb = None
+    for ids in chunks:
+        ctx2 = m(both[:, ids].cuda(), ov, ctx2)
+        ctxa = m(a[:, ids].cuda(), ov, ctxa)
+        ctxb = m(b[:, ids].cuda(), ov, ctxb)
+    torch.cuda.synchronize()
+    for key in ("chunk_sim3_alignment_enc", "frame_se3_alignment_enc"):
+        assert _rel(ctx2[key][:1], ctxa[key]) < 1e-5 and _rel(ctx2[key][1:], ctxb[key]) < 1e-5, key
+    for key in ("pose_enc", "depth"):
+        for x2, xa, xb in zip(ctx2[key], ctxa[key], ctxb[key]):
+            assert _rel(x2[:1], xa) < 1e-5 and _rel(x2[1:], xb) < 1e-5, key
