@@ -105,3 +105,56 @@ def test_gt_scale_alignments_match_reference(golden, name):
     for k in ("pose_enc", "depth", "world_points"):
         np.testing.assert_allclose(p[k].numpy(), g[f"{name}_{k}"], rtol=1e-6, atol=1e-6)
     np.testing.assert_allclose(np.asarray(p["alignment_scales"], dtype=np.float64), g[f"{name}_scales"], rtol=1e-6)
+
+
+def _sync_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(3)
+        pred = torch.eye(4).repeat(12, 1, 1)
+        pred[:, :3, 3] = torch.randn(12, 3, generator=g)
+        gt = torch.eye(4).repeat(12, 1, 1)
+        lo, hi = (0, 7) if rank == 0 else (7, 12)  # ragged shards
+        ate, rpe = AbsoluteTrajectoryError(), RelativePoseError()
+        ate.update(pred[lo:hi], gt[lo:hi])
+        rpe.update(pred[lo:hi], gt[lo:hi])
+        ate.sync()
+        rpe.sync()
+        if rank == 0:
+            q.put({**ate.compute(), **rpe.compute()})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_metric_sync_across_ranks():
+    """sync() = torchmetrics' dist_reduce_fx='cat': the two ragged shards
+    reduce to the metric over the concatenated error lists."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_sync_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    g = torch.Generator().manual_seed(3)
+    pred = torch.eye(4).repeat(12, 1, 1)
+    pred[:, :3, 3] = torch.randn(12, 3, generator=g)
+    gt = torch.eye(4).repeat(12, 1, 1)
+    ate, rpe = AbsoluteTrajectoryError(), RelativePoseError()
+    ate.update(pred, gt)
+    rpe.update(pred[:7], gt[:7])
+    rpe.update(pred[7:], gt[7:])
+    ref = {**ate.compute(), **rpe.compute()}
+    for k in ref:
+        assert abs(got[k] - ref[k]) < 1e-6, (k, got, ref)
