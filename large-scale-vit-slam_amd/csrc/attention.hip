@@ -132,6 +132,14 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
   bf16x8 qf[NKS];
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) qf[ks] = *(const bf16x8*)(qp + (int64_t)qr * a.ldq + ks * 16 + 8 * hl);
+  if constexpr ((VAR & 32) && !(VAR & 64)) {
+    // scores come out of the MFMA already in log2 units: Q * (scale log2 e),
+    // re-rounded to bf16 (one extra rounding of Q, ~2^-9 relative)
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[ks][j] = (__bf16)((float)qf[ks][j] * a.c);
+  }
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) asm volatile("" : "+v"(qf[ks]));  // retire the Q loads before the loop
 
@@ -182,8 +190,17 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
   f32x16 o[NDB];
 #pragma unroll
   for (int i = 0; i < NDB; ++i) o[i] = f32x16{};
-  float m_run = -INFINITY, l_run = 0.f;
+  // VAR & 32 starts from a finite "unset" offset: masked scores (-inf) minus
+  // it stay -inf (-inf - -inf would be a NaN, and the kernel is built with
+  // -fno-honor-nans, so a NaN could slip past the range guard)
+  constexpr float M_UNSET = -1e30f;
+  float m_run = (VAR & 32) ? M_UNSET : -INFINITY, l_run = 0.f;
   f32x16 lsum = f32x16{};  // VAR & 8: every row of the ones-block product holds l[q]
+  // VAR & 32: per-row bound exponent of the offset mode (60 at offset 0, THR
+  // once the row carries a max offset) and whether every row of the wave sits
+  // at offset 0 (then p = exp2(s) with no subtraction at all)
+  float lim = THR, limv = 256.0f;
+  bool zero_off = false;
   const float c = a.c;
   const int nt = (a.nk + BKV - 1) / BKV;
 
@@ -223,21 +240,119 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
     }
     return S2{{s[0], s[1]}};
   };
+  // ---- the same scores recomputed on a rare path (VAR & 32): the LDS offset
+  // goes through an empty asm so the reads are not CSE'd with the common
+  // path's (which would keep 32 K-fragment registers live across the tile)
+  // and the MFMAs cannot be speculated out of the branch
+  auto qk_again = [&](auto bufc) -> S2 {
+    constexpr int BUF = decltype(bufc)::value;
+    uint32_t opq = BUF * 2 * TILEB;
+    asm volatile("" : "+v"(opq));
+    const char* base = smem + opq;
+    f32x16 s[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      s[kb] = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const bf16x8 kf = *(const bf16x8*)(base + ka[ks] + kb * 32 * ROWB);
+        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kb], 0, 0, 0);
+      }
+    }
+    return S2{{s[0], s[1]}};
+  };
   // ---- mask, online softmax and O^T += V^T . P^T for the tile in slot BUF
-  auto soft_pv = [&](auto bufc, int t, S2 sc) {
+  auto soft_pv = [&](auto bufc, int t, S2 sc, auto zc) {
     constexpr int BUF = decltype(bufc)::value;
     const char* base = smem + BUF * 2 * TILEB;
     f32x16 s[2] = {sc.v[0], sc.v[1]};
     const int kv0 = t * BKV;
-    if (kv0 + BKV > a.nk) {
+    auto mask = [&]() {
+      if (kv0 + BKV > a.nk) {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+        for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kv0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-          if (key >= a.nk) s[kb][r] = -INFINITY;
-        }
-    }
+          for (int r = 0; r < 16; ++r) {
+            const int key = kv0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+            if (key >= a.nk) s[kb][r] = -INFINITY;
+          }
+      }
+    };
+    mask();
+    bf16x8 pf[2][2];
+    if constexpr (VAR & 32) {
+      // Offset-free online softmax.  softmax is shift-invariant, and bf16 / fp32
+      // keep their relative precision at any exponent, so the max subtraction
+      // only guards the exponent range.  Each row carries an offset m_run
+      // (log2 units), fixed at its first tile: 0 when that tile's max lies in
+      // [-60, 60] (then p = exp2(s) -- no max, no subtraction; the first
+      // tile's max term keeps l >= 2^-60), else the max itself.  A lane's
+      // partial sum over its 32 keys <= 2^lim bounds every p of it by 2^lim
+      // (lim = 60 at offset 0, THR otherwise -- the T13 bound), so no row max
+      // is computed on the common path.  Only when some lane's sum exceeds its
+      // bound (first tile: m_run = -inf -> p = inf) does the wave recompute the
+      // raw scores from LDS, take the true row max and move the offset of the
+      // rows that need it -- before this tile's P.V (the textbook order).
+      // VAR & 64: exact scores (s * c per element, no Q prescale).
+      float rs[4];
+      auto exps = [&](auto shc) {
+        constexpr bool shifted = decltype(shc)::value;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rs[i] = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int ss = 0; ss < 2; ++ss) {
+            bf16x8 t;  // whole-vector write: the previous pf is dead here, not an insert operand
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              float x = s[kb][8 * ss + j];
+              if constexpr (VAR & 64) x = shifted ? fmaf(x, c, -m_run) : x * c;
+              else if constexpr (shifted) x -= m_run;
+              const float p = __builtin_amdgcn_exp2f(x);
+              rs[0] += p;  // one chain: split sums get SLP-packed into v_pk_add_f32
+              t[j] = (__bf16)p;
+            }
+            pf[kb][ss] = t;
+          }
+      };
+      // zero-offset loop (zc true): p = exp2(s); a wave that has left offset 0
+      // (zero_off false: also before its first tile) takes the rare path
+      constexpr bool ZL = decltype(zc)::value;
+      exps(std::integral_constant<bool, !ZL>{});
+      float rsum = (rs[0] + rs[1]) + (rs[2] + rs[3]);
+      if (__builtin_amdgcn_ballot_w64(!(rsum <= limv) || (ZL && !zero_off)) != 0) {
+        const S2 raw = qk_again(bufc);
+        s[0] = raw.v[0];
+        s[1] = raw.v[1];
+        mask();
+        float mx = fmaxf(s[0][0], s[0][1]);
+#pragma unroll
+        for (int r = 2; r < 16; r += 2) mx = fmaxf(fmaxf(mx, s[0][r]), s[0][r + 1]);
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) mx = fmaxf(fmaxf(mx, s[1][r]), s[1][r + 1]);
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+        if constexpr (VAR & 64) mx *= c;
+        // a lane sum > 2^lim implies a p > 2^(lim-5): move the offset exactly
+        // for those rows (mx > m_run + lim - 5), so afterwards p <= 1 there and
+        // every other row still has p <= 2^(lim-5), sum <= 2^lim
+        float m_new = m_run;
+        if (m_run == M_UNSET) m_new = fabsf(mx) <= 60.f ? 0.f : mx;
+        else if (mx > m_run + (lim - 5.f)) m_new = mx;
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        m_run = m_new;
+        lim = m_run == 0.f ? 60.f : THR;
+        limv = m_run == 0.f ? 0x1p60f : 256.0f;  // 2^lim
+        zero_off = __builtin_amdgcn_ballot_w64(m_run != 0.f) == 0;
+        l_run *= alpha;
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) o[db] *= alpha;
+        exps(std::true_type{});
+        rsum = (rs[0] + rs[1]) + (rs[2] + rs[3]);
+      }
+      l_run += rsum;
+    } else {
     // ---- row max (lane-partial over 32 keys, then the partner half)
     float mx;
     if constexpr (VAR & 2) {
@@ -276,7 +391,6 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
       for (int db = 0; db < NDB; ++db) o[db] *= alpha;
     }
     float rs[4] = {0.f, 0.f, 0.f, 0.f};  // four partial row sums (short add chains)
-    bf16x8 pf[2][2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -288,6 +402,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
           pf[kb][ss][j] = (__bf16)p;
         }
     if constexpr (!(VAR & 8)) l_run += (rs[0] + rs[1]) + (rs[2] + rs[3]);
+    }
     // ---- O^T += V^T . P^T
 #pragma unroll
     for (int db = 0; db < NDB; ++db)
@@ -313,7 +428,6 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
     }
   };
 
-  auto tile = [&](auto bufc, int t) { soft_pv(bufc, t, qk(bufc)); };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
@@ -336,7 +450,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
       if (t + 2 < nt) stage(decltype(sf)::value, t + 2);
       S2 nxt = cur;
       if (t + 1 < nt) nxt = qk(sn);
-      soft_pv(sc, t, cur);
+      soft_pv(sc, t, cur, std::false_type{});
       cur = nxt;
     };
     for (int t = 0; t < nt; t += 3) {
@@ -350,16 +464,32 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
     stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int t = 0; t < nt; t += 2) {
-      if (t + 1 < nt) stage(1, t + 1);
-      tile(I0{}, t);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (t + 1 >= nt) break;
-      if (t + 2 < nt) stage(0, t + 2);
-      tile(I1{}, t + 1);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+    // VAR & 32: two copies of the tile loop, one per offset mode (one loop with
+    // a per-tile choice between the two exp forms costs ~25 VGPRs at the merge:
+    // occupancy 4 -> 3).  Every wave starts in the zero-offset loop and leaves
+    // it for good, at a tile pair boundary, once one of its rows took an offset.
+    auto run = [&](auto zc, int t0) -> int {
+      for (int t = t0; t < nt; t += 2) {
+        if (t + 1 < nt) stage(1, t + 1);
+        soft_pv(I0{}, t, qk(I0{}), zc);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t + 1 >= nt) break;
+        if (t + 2 < nt) stage(0, t + 2);
+        soft_pv(I1{}, t + 1, qk(I1{}), zc);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if constexpr (decltype(zc)::value) {
+          if (!zero_off) return t + 2;
+        }
+      }
+      return nt;
+    };
+    if constexpr (VAR & 32) {
+      const int t1 = run(std::true_type{}, 0);
+      if (t1 < nt) run(std::false_type{}, t1);
+    } else {
+      run(std::false_type{}, 0);
     }
   }
 
@@ -410,6 +540,23 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
     if (nw == 8) attn_fwd_kernel<64, 8, 19><<<nwg, 512, 0, s>>>(a);
     else if (g_vggt_attn_variant == 23) attn_fwd_kernel<64, 4, 23><<<nwg, 256, 0, s>>>(a);
     else attn_fwd_kernel<64, 4, 19><<<nwg, 256, 0, s>>>(a);
+    HIP_LAUNCH_CHECK();
+    return VGGT_OK;
+  }
+  if (g_vggt_attn_variant & 32) {  // offset-free softmax (bit 0 and the exact-score bit 64 combine)
+    const int v = (g_vggt_attn_variant & 1) + ((g_vggt_attn_variant & 64) ? 2 : 0);
+    switch ((D == 64 ? 0 : 8) + (nw == 8 ? 4 : 0) + v) {
+#define VGGT_ATTN_SCASE(DD, NWW, V)                                                               \
+  case (DD == 64 ? 0 : 8) + (NWW == 8 ? 4 : 0) + V:                                                \
+    attn_fwd_kernel<DD, NWW, 32 + (V & 1) + ((V & 2) ? 64 : 0)><<<nwg, NWW * 64, 0, s>>>(a); \
+    break;
+      VGGT_ATTN_SCASE(64, 4, 0) VGGT_ATTN_SCASE(64, 4, 1) VGGT_ATTN_SCASE(64, 4, 2) VGGT_ATTN_SCASE(64, 4, 3)
+      VGGT_ATTN_SCASE(64, 8, 0) VGGT_ATTN_SCASE(64, 8, 1) VGGT_ATTN_SCASE(64, 8, 2) VGGT_ATTN_SCASE(64, 8, 3)
+      VGGT_ATTN_SCASE(128, 4, 0) VGGT_ATTN_SCASE(128, 4, 1) VGGT_ATTN_SCASE(128, 4, 2) VGGT_ATTN_SCASE(128, 4, 3)
+      VGGT_ATTN_SCASE(128, 8, 0) VGGT_ATTN_SCASE(128, 8, 1) VGGT_ATTN_SCASE(128, 8, 2) VGGT_ATTN_SCASE(128, 8, 3)
+#undef VGGT_ATTN_SCASE
+      default: return VGGT_ERR_UNSUPPORTED;
+    }
     HIP_LAUNCH_CHECK();
     return VGGT_OK;
   }

@@ -16,7 +16,7 @@ int env_or(const char* name, int dflt) {
 
 int g_vggt_gemm_tile = env_or("VGGT_GEMM", -1);
 int g_vggt_attn_waves = env_or("VGGT_ATTN_WAVES", 4);
-int g_vggt_attn_variant = env_or("VGGT_ATTN_VARIANT", 3);
+int g_vggt_attn_variant = env_or("VGGT_ATTN_VARIANT", 33);
 
 extern "C" int vggt_tune(int knob, int value) {
   int prev;
@@ -32,7 +32,11 @@ extern "C" int vggt_tune(int knob, int value) {
       g_vggt_attn_waves = value;
       return prev;
     case VGGT_TUNE_ATTN_VARIANT:
-      if (value < 0 || (value > 15 && value != 19 && value != 23)) return VGGT_ERR_UNSUPPORTED;
+      // 0-15: bit combinations of the max-tracking kernel; 19/23: pipelined QK^T;
+      // 32/33 (+64 exact scores): offset-free softmax
+      if (value < 0 || (value > 15 && value != 19 && value != 23 && value != 32 && value != 33 && value != 96 &&
+                        value != 97))
+        return VGGT_ERR_UNSUPPORTED;
       prev = g_vggt_attn_variant;
       g_vggt_attn_variant = value;
       return prev;

@@ -157,7 +157,7 @@ def _ref_attn(q, k, v, scale):
     return torch.softmax(s, -1) @ v.float()
 
 
-@pytest.mark.parametrize("variant", [3, 11, 15, 19, 23])
+@pytest.mark.parametrize("variant", [3, 11, 15, 19, 23, 32, 97])
 @pytest.mark.parametrize("D,H,batch,n", [(64, 16, 3, 21), (64, 16, 2, 1374), (128, 8, 2, 1375), (64, 2, 1, 4100),
                                          (128, 2, 1, 64), (64, 1, 1, 1)])
 def test_attention_vs_torch(N, D, H, batch, n, variant):
@@ -214,7 +214,7 @@ def test_attention_global_shape_rows(N):
     assert _rel(o[rows], ref) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [3, 11, 19])
+@pytest.mark.parametrize("variant", [3, 11, 19, 32, 96])
 def test_attention_online_softmax_rescale(N, variant):
     """Force the running max to jump late (rule 26): one key with a huge score
     in the last tile for some rows."""
@@ -223,6 +223,52 @@ def test_attention_online_softmax_rescale(N, variant):
         _online_softmax_rescale(N)
     finally:
         N.tune(N.TUNE_ATTN_VARIANT, prev)
+
+
+@pytest.mark.parametrize("variant", [32, 33, 96, 97])
+@pytest.mark.parametrize("case", ["overflow_late", "all_negative", "huge_first_tile", "mixed_rows"])
+def test_attention_offset_free_extremes(N, variant, case):
+    """Offset-free softmax (VAR & 32): every branch of its range guard against
+    an fp64 host reference of the whole tensor (cdna_hip_programming.md §5.4
+    rule 26) -- rows whose scores overflow 2^60 only in a late tile, rows whose
+    first-tile max is below -60 or above +60 (offset rows), and a mix of offset
+    and zero-offset rows inside one wave."""
+    n, H, D = 700, 2, 64
+    C = H * D
+    g = torch.Generator().manual_seed(7)
+    q = torch.randn(n, C, generator=g) * 0.3
+    k = torch.randn(n, C, generator=g) * 0.3
+    v = torch.randn(n, C, generator=g)
+    if case == "overflow_late":      # score ~ +1100 (log2 units ~ +200) at key 650
+        q[:40] = 4.0
+        k[650] = 4.0
+    elif case == "all_negative":     # every score ~ -900 for the first rows
+        q[:64] = 4.0
+        k[:] = -3.5 + 0.05 * torch.randn(n, C, generator=g)
+    elif case == "huge_first_tile":  # key 3 dominates from the first tile on
+        q[:64] = 4.0
+        k[3] = 4.0
+    else:                            # alternate rows: offset / zero-offset in one wave
+        q[0:128:2] = 4.0
+        k[10] = 4.0
+        k[600] = 4.5
+    qkv = torch.cat([q, k, v], 1).to(torch.bfloat16)
+    prev = N.tune(N.TUNE_ATTN_VARIANT, variant)
+    try:
+        qkv_d = qkv.cuda()
+        o = torch.empty(n, C, device="cuda", dtype=torch.bfloat16)
+        N.attention(qkv_d[:, :C], qkv_d[:, C:2 * C], qkv_d[:, 2 * C:], o, 1, H, n, n, D, n, n, n)
+        torch.cuda.synchronize()
+    finally:
+        N.tune(N.TUNE_ATTN_VARIANT, prev)
+    t = qkv.double().view(1, n, 3, H, D).permute(2, 0, 3, 1, 4)
+    ref = _ref_attn(t[0], t[1], t[2], D ** -0.5).permute(0, 2, 1, 3).reshape(n, C)
+    got = o.double().cpu()
+    assert torch.isfinite(got).all()
+    assert _rel(got, ref) < 1e-2, _rel(got, ref)
+    # per-row check: no row may be silently wrong (a bad rescale hits whole rows)
+    row_err = (got - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-6)
+    assert row_err.max() < 5e-2, row_err.max()
 
 
 def _online_softmax_rescale(N):
