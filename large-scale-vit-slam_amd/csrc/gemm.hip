@@ -54,16 +54,19 @@ template <int EPI, int BM, int BN, int NT, int CROW>
 __device__ __forceinline__ void write_tile(const char* Cs, int m0, int n0, int M, const Epi& ep,
                                            const float* tcs = nullptr, const float* tsn = nullptr) {
   constexpr int CPR = BN / 8;        // 16-B chunks per row
-  constexpr int RPP = NT / CPR;      // rows per pass
+  constexpr int RPP = NT / CPR;      // rows per pass (NT % CPR threads idle when BN = 192)
   const int ch = threadIdx.x % CPR;
   const int n = n0 + ch * 8;
+  if (threadIdx.x >= RPP * CPR) return;
   float g[8];
   // EPI_QKNORM: this thread's 8 norm weights / biases (fixed column), RoPE
-  // tables from LDS when the caller staged them there
+  // tables from LDS when the caller staged them there.  The q / k / v region
+  // is per thread: a 192-wide tile can straddle a region boundary (heads and
+  // regions are multiples of 64 columns, so a head never does).
   float nwv[8], nbv[8];
   if constexpr (EPI == EPI_QKNORM_D64 || EPI == EPI_QKNORM_D128) {
     constexpr int D = EPI == EPI_QKNORM_D64 ? 64 : 128;
-    const int region = n0 / ep.hd;
+    const int region = n / ep.hd;
     const int e0 = (n % ep.hd) % D;
     const float* nw = region ? ep.kw : ep.qw;
     const float* nb = region ? ep.kb : ep.qb;
@@ -87,8 +90,7 @@ __device__ __forceinline__ void write_tile(const char* Cs, int m0, int n0, int M
     }
   }
 #pragma unroll 2
-  for (int it = 0; it < BM / RPP; ++it) {
-    const int ml = it * RPP + threadIdx.x / CPR;
+  for (int ml = threadIdx.x / CPR; ml < BM; ml += RPP) {
     const int m = m0 + ml;
     if (m >= M) continue;
     const uint4 cv = *(const uint4*)(Cs + ml * CROW + ch * 16);
@@ -100,7 +102,7 @@ __device__ __forceinline__ void write_tile(const char* Cs, int m0, int n0, int M
       // end -- the arithmetic of headnorm_rope_kernel (norm.hip), in registers.
       constexpr int D = EPI == EPI_QKNORM_D64 ? 64 : 128;
       constexpr int LPH = D / 8;  // lanes per head (consecutive: ch is the low index)
-      const int region = n0 / ep.hd;  // 0 q, 1 k, 2 v -- uniform per block
+      const int region = n / ep.hd;  // 0 q, 1 k, 2 v
       if (region >= 2) {
         *(uint4*)((bf16_t*)ep.out + (int64_t)m * ep.ldo + n) = cv;
         continue;
@@ -504,6 +506,219 @@ int launch_ring(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int 
   return VGGT_OK;
 }
 
+// ===========================================================================
+// Ping-pong form: 256 x BN block tile (BN = 256 / 192 / 128), BK = 64, two
+// LDS buffers filled by LDS-DMA, 8 waves as 2 (M) x 4 (N); wave (wm, wn) owns
+// rows wm*128.. and columns wn*BN/4.. of the tile.  Each K-tile is two
+// k-steps; per k-step a wave runs a READ segment (its fragments for the step
+// from LDS -- and, on the first step, the DMA of the next K-tile) and a MATH
+// segment (8 x BN/64 MFMAs), separated by workgroup barriers.  The two M
+// halves are staggered by one barrier (waves 4-7 start with an extra one),
+// and each SIMD holds one wave of each half, so on every SIMD one wave's
+// MFMAs run beside the other wave's LDS reads (cdna_hip_programming.md §5,
+// "256² 8-phase template"; MI355X_MICROARCH.md "Two waves per SIMD").
+//
+// LDS hazards (two buffers, K-tile kt in buffer kt & 1):
+//  * WAR: the DMA of K-tile kt+1 is issued in READ(kt, 0).  The last reads of
+//    its buffer are READ(kt-1, 1) of both halves, each ending with
+//    lgkmcnt(0) before its barrier; READ(kt, 0) of a half starts after the
+//    barrier that ends the other half's READ(kt-1, 1).
+//  * RAW: every wave waits vmcnt(0) for its own DMA at the end of READ(kt, 1)
+//    (before that segment's barrier); READ(kt+1, 0) of either half starts at
+//    least one barrier later.
+// ===========================================================================
+constexpr int PBM = 256, PBK = 64, PNT = 512;
+
+template <int BN>
+struct PPCfg {
+  static constexpr int WN = BN / 4;               // wave tile columns
+  static constexpr int NI = WN / 16;              // 16-column fragments per wave
+  static constexpr int MI = 8;                    // 16-row fragments per wave (128 rows)
+  static constexpr int ABYTES = PBM * PBK * 2;    // 32 KiB
+  static constexpr int WBYTES = BN * PBK * 2;
+  static constexpr int BUF = ABYTES + WBYTES;
+  static constexpr int AL = ABYTES / 1024 / 8;    // LDS-DMA instructions per wave per K-tile (A)
+  static constexpr int WL = WBYTES / 1024 / 8;    // (W)
+  static constexpr int CROW = BN * 2 + 16;
+  static constexpr int LDS = (2 * BUF > PBM * CROW) ? 2 * BUF : PBM * CROW;
+};
+
+template <int EPI, int BN>
+__global__ __launch_bounds__(PNT, 1) void gemm_pp_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                         const bf16_t* __restrict__ W, int64_t ldw, int M, int N,
+                                                         int K, Epi ep) {
+  using C = PPCfg<BN>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tiles_n = N / BN;
+  const int tiles_m = (M + PBM - 1) / PBM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (t / tiles_n) * PBM;
+  const int n0 = (t % tiles_n) * BN;
+  const int nk = K / PBK;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // ---- LDS-DMA: piece p (1 KiB) of an operand image = rows 8p..8p+7 (128-B
+  // rows); lane -> row 8p + lane/8, 16-B chunk lane%8 XOR-swizzled on the
+  // source (the DMA image is lane-linear); rows past M clamp to M-1.
+  const int32x4 ra = make_rsrc_u(A + (int64_t)m0 * lda);
+  const int32x4 rw = make_rsrc_u(W + (int64_t)n0 * ldw);
+  uint32_t aoff[C::AL], woff[C::WL];
+#pragma unroll
+  for (int i = 0; i < C::AL; ++i) {
+    const int row = (wave * C::AL + i) * 8 + (lane >> 3);
+    const int rr = min(m0 + row, M - 1) - m0;
+    aoff[i] = (uint32_t)(rr * lda + ((lane & 7) ^ (row & 7)) * 8) * 2u;
+  }
+#pragma unroll
+  for (int i = 0; i < C::WL; ++i) {
+    const int row = (wave * C::WL + i) * 8 + (lane >> 3);
+    woff[i] = (uint32_t)(row * ldw + ((lane & 7) ^ (row & 7)) * 8) * 2u;
+  }
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem));
+  auto stage = [&](int buf, int kt) {
+    const uint32_t b = lds0 + buf * C::BUF;
+    const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(kt * PBK * 2));
+#pragma unroll
+    for (int i = 0; i < C::AL; ++i) dma16s(ra, aoff[i], soff, b + (wave * C::AL + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < C::WL; ++i) dma16s(rw, woff[i], soff, b + C::ABYTES + (wave * C::WL + i) * 1024);
+  };
+
+  // ---- fragment read offsets: row & 7 == lane & 7, so the swizzled chunk of
+  // k-step ks is lane-only; everything else is an immediate
+  const int fr = lane & 15, fc = lane >> 4;
+  uint32_t a_off[2], w_off[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const uint32_t sw = (uint32_t)(((ks * 4 + fc) ^ (fr & 7)) << 4);
+    a_off[ks] = (wm * 128 + fr) * 128 + sw;
+    w_off[ks] = C::ABYTES + (wn * C::WN + fr) * 128 + sw;
+  }
+
+  f32x4 acc[C::NI][C::MI];
+#pragma unroll
+  for (int i = 0; i < C::NI; ++i)
+#pragma unroll
+    for (int j = 0; j < C::MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[C::MI], wf[C::NI];
+
+  auto read_frags = [&](int buf, int ks) {
+    const char* base = smem + buf * C::BUF;
+#pragma unroll
+    for (int i = 0; i < C::NI; ++i) wf[i] = *(const bf16x8*)(base + w_off[ks] + i * 16 * 128);
+#pragma unroll
+    for (int i = 0; i < C::MI; ++i) af[i] = *(const bf16x8*)(base + a_off[ks] + i * 16 * 128);
+  };
+  auto math = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mi = 0; mi < C::MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < C::NI; ++ni)
+        acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], af[mi], acc[ni][mi], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  if (wm == 1) asm volatile("s_barrier" ::: "memory");  // stagger the second M half by one segment
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    // READ(kt, 0): next K-tile's DMA into the other buffer, this step's fragments
+    if (kt + 1 < nk) stage(buf ^ 1, kt + 1);
+    read_frags(buf, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    math();  // MATH(kt, 0)
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    // READ(kt, 1); own DMA of K-tile kt+1 retired before the barrier
+    read_frags(buf, 1);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    math();  // MATH(kt, 1)
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+  }
+  if (wm == 0) asm volatile("s_barrier" ::: "memory");  // balance the stagger
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  // ---- epilogue 1: acc (C^T fragments) + bias -> bf16 C tile in LDS ----
+  char* Cs = smem;
+#pragma unroll
+  for (int ni = 0; ni < C::NI; ++ni) {
+    const int nl = wn * C::WN + ni * 16 + 4 * (lane >> 4);
+    const f32x4 bv = *(const f32x4*)(ep.bias + n0 + nl);
+#pragma unroll
+    for (int mi = 0; mi < C::MI; ++mi) {
+      const int ml = wm * 128 + mi * 16 + (lane & 15);
+      uint2 pk;
+      pk.x = pack_bf2(acc[ni][mi][0] + bv[0], acc[ni][mi][1] + bv[1]);
+      pk.y = pack_bf2(acc[ni][mi][2] + bv[2], acc[ni][mi][3] + bv[3]);
+      *(uint2*)(Cs + ml * C::CROW + nl * 2) = pk;
+    }
+  }
+  __syncthreads();
+  if constexpr (EPI == EPI_QKNORM_D64 || EPI == EPI_QKNORM_D128) {
+    constexpr int D = EPI == EPI_QKNORM_D64 ? 64 : 128;
+    const int rd = ep.rope_mode == VGGT_ROPE_2D ? D / 2 : D;
+    const int tab = ep.rope_mode != VGGT_ROPE_NONE ? ep.tab_len * rd : 0;
+    float* ts = (float*)(smem + PBM * C::CROW);
+    if (tab > 0 && n0 < 2 * ep.hd && PBM * C::CROW + 2 * tab * 4 <= C::LDS) {
+      for (int i = threadIdx.x; i < tab; i += PNT) {
+        ts[i] = ep.cs[i];
+        ts[tab + i] = ep.sn[i];
+      }
+      __syncthreads();
+      write_tile<EPI, PBM, BN, PNT, C::CROW>(Cs, m0, n0, M, ep, ts, ts + tab);
+      return;
+    }
+  }
+  write_tile<EPI, PBM, BN, PNT, C::CROW>(Cs, m0, n0, M, ep);
+}
+
+template <int EPI, int BN>
+int launch_pp(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int M, int N, int K, const Epi& ep,
+              hipStream_t s) {
+  using C = PPCfg<BN>;
+  static bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              C::LDS);
+    return true;
+  }();
+  (void)attr;
+  const int nwg = ((M + PBM - 1) / PBM) * (N / BN);
+  gemm_pp_kernel<EPI, BN><<<nwg, PNT, C::LDS, s>>>(a, lda, w, ldw, M, N, K, ep);
+  return VGGT_OK;
+}
+
+// Ping-pong tile width for an N-wide output: the BN whose whole rounds of
+// 256-row tiles over the CUs cost least (per-tile time ~ BN), larger BN on a
+// tie; 192 only where the epilogue allows it.
+inline int pp_pick_bn(int M, int N, bool allow192) {
+  static int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    return n;
+  }();
+  const int tm = (M + PBM - 1) / PBM;
+  int best = 0;
+  long best_cost = 0;
+  for (int bn : {256, 192, 128}) {
+    if (N % bn || (bn == 192 && !allow192)) continue;
+    const long rounds = ((long)tm * (N / bn) + cus - 1) / cus;
+    const long cost = rounds * bn;
+    if (best == 0 || cost < best_cost) {
+      best = bn;
+      best_cost = cost;
+    }
+  }
+  return best;
+}
+
 }  // namespace
 
 extern "C" int vggt_gemm_bf16(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int M, int N,
@@ -524,12 +739,41 @@ extern "C" int vggt_gemm_bf16(const void* A, int64_t lda, const void* W, int64_t
   // up-projection (N >= 4096: fc1, 256 vs 278 us in the aggregator run r1i), the
   // 128x128 form elsewhere (qkv N = 3072: 154 vs 165 us; N = 1024 proj / fc2,
   // where 256x256 tiles leave the last of only ~1.3 rounds of workgroups idle).
+  // Auto (-1), from scripts/kbench.py on the aggregator shapes (r1s): the
+  // ping-pong form with 256-wide tiles for fc1 (229 vs 244 us ring) and fc2
+  // (218 vs 223 us 128x128), 128-wide for the 1024x1024 projection (73 vs
+  // 75 us); the 128x128 form for small M.
   int mode = g_vggt_gemm_tile;
-  if (mode < 0) mode = (N >= 4096 && N % 256 == 0 && M >= 1024) ? 1 : 0;
+  if (mode < 0) {
+    if (M >= 4096 && K % PBK == 0 && N % 128 == 0)
+      mode = (N % 256 == 0 && (int64_t)N * K >= (1 << 22)) ? 4 : 6;
+    else
+      mode = 0;
+  }
+  if (mode >= 3 && K % PBK) mode = 2;    // the ping-pong form steps K by 64
   if (mode == 0 && K % BK) mode = 2;     // the 128x128 form steps K by 64
   if (mode == 1 && N % 256) mode = 2;
   // per-lane 32-bit DMA offsets span one 256-row panel
   if (mode != 0 && (int64_t)RBM * (lda > ldw ? lda : ldw) * 2 >= (1ll << 31)) return VGGT_ERR_SHAPE;
+  if (mode >= 3) {
+    int bn = mode == 4 ? 256 : mode == 5 ? 192 : mode == 6 ? 128 : pp_pick_bn(M, N, true);
+    if (bn == 0 || N % bn) bn = pp_pick_bn(M, N, true);
+    if (bn == 0) return VGGT_ERR_SHAPE;
+#define VGGT_PP(E)                                                    \
+  (bn == 256   ? launch_pp<E, 256>(a, lda, w, ldw, M, N, K, ep, s)   \
+   : bn == 192 ? launch_pp<E, 192>(a, lda, w, ldw, M, N, K, ep, s)   \
+               : launch_pp<E, 128>(a, lda, w, ldw, M, N, K, ep, s))
+    switch (epi) {
+      case VGGT_EPI_BF16: VGGT_PP(VGGT_EPI_BF16); break;
+      case VGGT_EPI_GELU_BF16: VGGT_PP(VGGT_EPI_GELU_BF16); break;
+      case VGGT_EPI_RESID_F32: VGGT_PP(VGGT_EPI_RESID_F32); break;
+      case VGGT_EPI_F32: VGGT_PP(VGGT_EPI_F32); break;
+      default: return VGGT_ERR_UNSUPPORTED;
+    }
+#undef VGGT_PP
+    HIP_LAUNCH_CHECK();
+    return VGGT_OK;
+  }
   if (mode == 1) {
     switch (epi) {
       case VGGT_EPI_BF16: launch_ring<VGGT_EPI_BF16, 256>(a, lda, w, ldw, M, N, K, ep, s); break;
@@ -582,10 +826,30 @@ extern "C" int vggt_gemm_qkv(const void* A, int64_t lda, const void* W, int64_t 
   hipStream_t s = (hipStream_t)stream;
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* w = (const bf16_t*)W;
-  int mode = g_vggt_gemm_tile < 0 ? 0 : g_vggt_gemm_tile;  // auto: the 128x128 form (measured faster for qkv)
+  // auto: the 256-wide ping-pong form on long M (fused qkv 179 vs 239 us for the
+  // 128x128 form, r1s), the 128x128 form otherwise
+  int mode = g_vggt_gemm_tile;
+  if (mode < 0) mode = (M >= 4096 && K % PBK == 0) ? (N % 256 == 0 ? 4 : 6) : 0;
+  if (mode >= 3 && K % PBK) mode = 2;
   if (mode == 0 && K % BK) mode = 2;
   if (mode == 1 && hd % 256) mode = 2;
   if (mode != 0 && (int64_t)RBM * (lda > ldw ? lda : ldw) * 2 >= (1ll << 31)) return VGGT_ERR_SHAPE;
+  if (mode >= 3) {
+    // 192-wide tiles only with 64-wide heads (the norm's lane groups stay aligned)
+    int bn = mode == 4 ? 256 : mode == 5 ? 192 : mode == 6 ? 128 : pp_pick_bn(M, N, D == 64);
+    if (bn == 0 || N % bn || (bn == 192 && D != 64)) bn = pp_pick_bn(M, N, D == 64);
+    if (bn == 0) return VGGT_ERR_SHAPE;
+    if (D == 64) {
+      if (bn == 256) launch_pp<EPI_QKNORM_D64, 256>(a, lda, w, ldw, M, N, K, ep, s);
+      else if (bn == 192) launch_pp<EPI_QKNORM_D64, 192>(a, lda, w, ldw, M, N, K, ep, s);
+      else launch_pp<EPI_QKNORM_D64, 128>(a, lda, w, ldw, M, N, K, ep, s);
+    } else {
+      if (bn == 256) launch_pp<EPI_QKNORM_D128, 256>(a, lda, w, ldw, M, N, K, ep, s);
+      else launch_pp<EPI_QKNORM_D128, 128>(a, lda, w, ldw, M, N, K, ep, s);
+    }
+    HIP_LAUNCH_CHECK();
+    return VGGT_OK;
+  }
   if (mode == 0) {
     const int nwg = ((M + BM - 1) / BM) * (N / BN);
     if (D == 64) gemm_bf16_kernel<EPI_QKNORM_D64><<<nwg, NT, 0, s>>>(a, lda, w, ldw, M, N, K, ep);

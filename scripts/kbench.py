@@ -66,6 +66,16 @@ def main():
             us = timeit(lambda: N.gemm_bf16(a, w, bias, out, epi, gamma=gamma), args.reps)
             res[f"{name}/tile{mode}"] = {"us": round(us, 1), "tflops": round(2 * M * Nn * K / us / 1e6, 1)}
             print(f"{name}/tile{mode}", res[f"{name}/tile{mode}"], flush=True)
+            if name == "qkv":  # the production form: q/k LayerNorm + RoPE2D in the epilogue
+                yy, xx = torch.meshgrid(torch.arange(37), torch.arange(37), indexing="ij")
+                pos = torch.cat([torch.zeros(5, 2, dtype=torch.long),
+                                 torch.stack([yy.reshape(-1), xx.reshape(-1)], -1) + 1], 0)
+                rp = RopeTables(pos, D, 100.0, dev)
+                qw, qb, kw, kb = (torch.rand(D, device=dev) for _ in range(4))
+                us = timeit(lambda: N.gemm_qkv(a, w, bias, out, H, D, qw, qb, kw, kb, 1e-5, rp.mode, rp.pos, rp.period,
+                                               rp.cos, rp.sin), args.reps)
+                res[f"qkv_fused/tile{mode}"] = {"us": round(us, 1), "tflops": round(2 * M * Nn * K / us / 1e6, 1)}
+                print(f"qkv_fused/tile{mode}", res[f"qkv_fused/tile{mode}"], flush=True)
     if "norm" in only:
         xf = torch.randn(M, C, device=dev)
         y = torch.empty(M, C, device=dev, dtype=torch.bfloat16)

@@ -62,8 +62,9 @@ def test_gemm_epilogues(N, M, Nn, K, epi):
         assert _rel(out, refb) < 4e-3
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2])
-@pytest.mark.parametrize("M,Nn,K", [(300, 256, 96), (1000, 768, 1024), (2300, 1024, 4096), (21984, 1024, 1024)])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("M,Nn,K", [(300, 256, 96), (1000, 768, 1024), (2300, 1024, 4096), (21984, 1024, 1024),
+                                    (5000, 3072, 1024)])
 @pytest.mark.parametrize("epi", [0, 1, 2])
 def test_gemm_tile_variants(N, mode, M, Nn, K, epi):
     """Every tile form (vggt_tune VGGT_TUNE_GEMM_TILE) on shapes that exercise
@@ -287,7 +288,7 @@ def _online_softmax_rescale(N):
     assert _rel(o, ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("D,H,mode,norm", [(64, 16, 1, True), (64, 16, 0, True), (128, 8, 1, True), (128, 8, 2, True),
                                            (64, 4, 1, False)])
 def test_gemm_qkv_fused_matches_two_pass(N, tile, D, H, mode, norm):
