@@ -739,17 +739,15 @@ extern "C" int vggt_gemm_bf16(const void* A, int64_t lda, const void* W, int64_t
   // up-projection (N >= 4096: fc1, 256 vs 278 us in the aggregator run r1i), the
   // 128x128 form elsewhere (qkv N = 3072: 154 vs 165 us; N = 1024 proj / fc2,
   // where 256x256 tiles leave the last of only ~1.3 rounds of workgroups idle).
-  // Auto (-1), from scripts/kbench.py on the aggregator shapes (r1s): the
-  // ping-pong form with 256-wide tiles for fc1 (229 vs 244 us ring) and fc2
-  // (218 vs 223 us 128x128), 128-wide for the 1024x1024 projection (73 vs
-  // 75 us); the 128x128 form for small M.
+  // Auto (-1), from the in-model kernel tables (profiles/r1s_*): the ping-pong
+  // form with 256-wide tiles for the wide bf16-output projections (fc1 with
+  // GELU 234 vs 240 us ring, plain qkv 146 vs 191 us); the 128x128 form (two
+  // workgroups per CU, so one's fp32 residual read-modify-write overlaps the
+  // other's MFMAs) for the LayerScale+residual projections (proj 83 vs 90 us,
+  // fc2 225 vs 234 us) and for small M.
   int mode = g_vggt_gemm_tile;
-  if (mode < 0) {
-    if (M >= 4096 && K % PBK == 0 && N % 128 == 0)
-      mode = (N % 256 == 0 && (int64_t)N * K >= (1 << 22)) ? 4 : 6;
-    else
-      mode = 0;
-  }
+  if (mode < 0)
+    mode = (M >= 4096 && K % PBK == 0 && N % 256 == 0 && N >= 2048 && epi != VGGT_EPI_RESID_F32) ? 4 : 0;
   if (mode >= 3 && K % PBK) mode = 2;    // the ping-pong form steps K by 64
   if (mode == 0 && K % BK) mode = 2;     // the 128x128 form steps K by 64
   if (mode == 1 && N % 256) mode = 2;
