@@ -289,6 +289,125 @@ int vggt_sim3_points(const float* pts, int64_t p_bs, int B, int64_t n, const flo
  * featureAligned_vggt.py:171; pointAligned_wrapped_vggt.py:130-132). */
 int vggt_scale_f32(float* x, int64_t bs, int B, int64_t n, const float* scale, void* stream);
 
+/* ======================================================================
+ * Training (backward) entry points -- alignment-head training, SURVEY.md §8f
+ * row 4: train_featureAlignedVGGT_vkitti.yaml freezes the aggregator, camera
+ * and depth heads (:80-83) and trains AlignmentHead (alignment_head.py) under
+ * bf16-mixed autocast (run_model.py:472), with checkpoint()-recomputed blocks
+ * (alignment_head.py:351-426).  Gradients of bf16 tensors are bf16 (what
+ * autocast produces), parameter gradients fp32.  Column / row reductions
+ * into parameter gradients are deterministic: fixed row chunks write partial
+ * sums to `ws` (>= the size the matching *_workspace_bytes returns) and a
+ * second pass ADDS them, in chunk order, to the fp32 gradient buffer.
+ * ====================================================================== */
+
+/* Forward attention as vggt_attention_fwd (exact scores, no Q prescale) that
+ * also stores lse[(b*heads + h)*nq + q] = log2 sum_k exp2(q.k * scale * log2 e),
+ * consumed by vggt_attention_bwd (recompute of the frame blocks' SDPA). */
+int vggt_attention_fwd_lse(const void* q, int64_t ldq, int64_t q_bstride, const void* k, int64_t ldk,
+                           int64_t k_bstride, const void* v, int64_t ldv, int64_t v_bstride, void* o, int64_t ldo,
+                           int64_t o_bstride, float* lse, int batch, int heads, int nq, int nk, int D, float scale,
+                           void* stream);
+
+/*
+ * Flash-attention backward (bf16, D in {64,128}; F.scaled_dot_product_attention
+ * backward in vggt Attention, ext, called by the alignment head's frame blocks).
+ * q/k/v/o/dout strided as vggt_attention_fwd (v shares k's batch stride, dout
+ * shares o's layout); lse from vggt_attention_fwd_lse; delta: fp32
+ * [batch*heads*nq] scratch (written).  Writes bf16 dq [.., lddq] (q's batch
+ * stride) and dk, dv [.., lddkv] (k's batch stride), e.g. straight into the
+ * dqkv buffer laid out like qkv.
+ */
+int vggt_attention_bwd(const void* q, int64_t ldq, int64_t q_bstride, const void* k, int64_t ldk, int64_t k_bstride,
+                       const void* v, int64_t ldv, const void* o, const void* dout, int64_t ldo, int64_t o_bstride,
+                       const float* lse, float* delta, void* dq, int64_t lddq, void* dk, void* dv, int64_t lddkv,
+                       int batch, int heads, int nq, int nk, int D, float scale, void* stream);
+
+/*
+ * Small-window attention backward (vggt_attention_small's shapes: temporal
+ * cross attention, cross_attention.py:64-75, and the fp32 decoder blocks):
+ * one wave per (batch, head), recomputes P; dtype for every operand.
+ * dq [.., lddq] batch stride dq_bstride; dk, dv [.., lddkv] batch stride
+ * dkv_bstride.  Needs (2*nq*D + 2*nk*D + 2*nq*nk)*4 <= 64 KiB.
+ */
+int vggt_attention_small_bwd(const void* q, int64_t ldq, int64_t q_bstride, const void* k, int64_t ldk,
+                             int64_t k_bstride, const void* v, int64_t ldv, const void* dout, int64_t ldo,
+                             int64_t o_bstride, void* dq, int64_t lddq, int64_t dq_bstride, void* dk, void* dv,
+                             int64_t lddkv, int64_t dkv_bstride, int dtype, int batch, int heads, int nq, int nk, int D,
+                             float scale, void* stream);
+
+/*
+ * LayerNorm backward (nn.LayerNorm / F.layer_norm backward; every norm of the
+ * alignment head): x = the forward input, dy the output gradient, same row
+ * map as vggt_layernorm_grouped (logical row r -> group r/group; x and dx rows
+ * g*x_group_stride + x_row_offset + i, dy rows g*y_group_stride +
+ * y_row_offset + i).  dx (+)= (accumulate: f32 only).  dw/db (may be NULL)
+ * get the parameter gradients added.  C % 256 == 0, C <= 1024.
+ */
+size_t vggt_layernorm_bwd_workspace_bytes(int M, int C);
+int vggt_layernorm_bwd(const void* x, int xdtype, int64_t ldx, const float* w, float eps, const void* dy, int dydtype,
+                       int64_t ldy, void* dx, int dxdtype, int64_t lddx, int accumulate, int M, int C, int group,
+                       int x_group_stride, int x_row_offset, int y_group_stride, int y_row_offset, float* dw,
+                       float* db, void* ws, size_t ws_bytes, void* stream);
+
+/*
+ * Per-head LayerNorm + RoPE backward (q_norm/k_norm + rope of vggt Attention,
+ * ext, and CrossAttention, cross_attention.py:59-62): pre = the bf16/f32
+ * values before the norm (the linear's output), grad = d(output) in, d(pre)
+ * out, in place.  Heads [0, hsplit) use w0 (gradients into dw0/db0), heads
+ * [hsplit, H) use w1 (dw1/db1); NULL w = no norm.  RoPE conventions as
+ * vggt_headnorm_rope.
+ */
+size_t vggt_headnorm_rope_bwd_workspace_bytes(int M, int D);
+int vggt_headnorm_rope_bwd(const void* pre, int64_t ldp, void* grad, int64_t ldg, int dtype, int M, int H, int hsplit,
+                           int D, const float* w0, const float* w1, float eps, int rope_mode, const int32_t* pos,
+                           int period, const float* cos_tab, const float* sin_tab, int tab_len, float* dw0,
+                           float* db0, float* dw1, float* db1, void* ws, size_t ws_bytes, void* stream);
+
+/* Column-reduction workspace for vggt_colsum / vggt_layerscale_bwd / vggt_gelu_bwd. */
+size_t vggt_colred_workspace_bytes(int M, int N);
+
+/* out[n] (+)= sum_m x[m, n]  (Linear bias gradients).  N % 4 == 0. */
+int vggt_colsum(const void* x, int dtype, int64_t ldx, int M, int N, float* out, int accumulate, void* ws,
+                size_t ws_bytes, void* stream);
+
+/*
+ * LayerScale + residual backward (x + gamma * branch, vggt layers/block.py /
+ * cross_attention.py:130-131): dbranch = gamma * dout (rounded to odtype),
+ * dgamma += sum_m dout * branch, dbias += sum_m dbranch (the bias gradient of
+ * the Linear that produced the branch).  dgamma / dbias may be NULL.
+ */
+int vggt_layerscale_bwd(const float* dout, int64_t ldd, const void* branch, int bdtype, int64_t ldb,
+                        const float* gamma, void* dbranch, int odtype, int64_t ldo, int M, int N, float* dgamma,
+                        float* dbias, void* ws, size_t ws_bytes, void* stream);
+
+/* y = GELU(x) (exact erf), any f32/bf16 combination (Mlp.act, unfused training form). */
+int vggt_gelu_fwd(const void* x, int xdtype, int64_t ldx, void* y, int ydtype, int64_t ldy, int M, int N,
+                  void* stream);
+
+/* dpre = dh * GELU'(pre) (rounded to odtype); dbias += sum_m dpre (fc1 bias gradient; may be NULL). */
+int vggt_gelu_bwd(const void* dh, int dhdtype, int64_t lddh, const void* pre, int predtype, int64_t ldp, void* dpre,
+                  int odtype, int64_t ldo, int M, int N, float* dbias, void* ws, size_t ws_bytes, void* stream);
+
+/* x_f32[m, n] += gamma[n] * branch[m, n]  (LayerScale residual add with a saved branch). */
+int vggt_resid_scale_add(float* x, int64_t ldx, const void* branch, int bdtype, int64_t ldb, const float* gamma, int M,
+                         int N, void* stream);
+
+/* dst[c, r] = src[r, c] for 2-byte elements; columns r in [rows, rows_pad) of dst are zero
+ * (weight-gradient GEMM operands: dW = dY^T X as vggt_gemm_bf16(dY^T, X^T)). */
+int vggt_transpose_b16(const void* src, int64_t lds, int rows, int cols, void* dst, int64_t ldd, int rows_pad,
+                       void* stream);
+
+/* dW[n, k] (+)= sum_m dY[m, n] X[m, k]  fp32 (skinny-M decoder / gated-update Linear weight gradients). */
+int vggt_wgrad_f32(const float* dy, int64_t ldy, const float* x, int64_t ldx, int M, int N, int K, float* dw,
+                   int64_t ldw, int accumulate, void* stream);
+
+/* out[b] = sum_{i<n} a[b*bs + i] * c[b*bs + i]  (d chunk_scale of depth *= chunk_scale,
+ * featureAligned_vggt.py:171, in training).  ws >= vggt_batch_dot_workspace_bytes(B, n). */
+size_t vggt_batch_dot_workspace_bytes(int B, int64_t n);
+int vggt_batch_dot_f32(const float* a, const float* c, int64_t bs, int B, int64_t n, float* out, void* ws,
+                       size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

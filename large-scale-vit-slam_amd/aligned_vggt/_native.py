@@ -57,7 +57,29 @@ _SIGS = {
                        ctypes.c_size_t, _vp],
     "vggt_sim3_points": [_vp, _i64, _i, _i64, _vp, _vp, _vp, _i64, _vp],
     "vggt_scale_f32": [_vp, _i64, _i, _i64, _vp, _vp],
+    # training (backward) entry points
+    "vggt_attention_fwd_lse": [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i, _i, _i,
+                               _i, _i, _f, _vp],
+    "vggt_attention_bwd": [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _i64,
+                           _vp, _vp, _i64, _i, _i, _i, _i, _i, _f, _vp],
+    "vggt_attention_small_bwd": [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp,
+                                 _vp, _i64, _i64, _i, _i, _i, _i, _i, _i, _f, _vp],
+    "vggt_layernorm_bwd": [_vp, _i, _i64, _vp, _f, _vp, _i, _i64, _vp, _i, _i64, _i, _i, _i, _i, _i, _i, _i, _i, _vp,
+                           _vp, _vp, ctypes.c_size_t, _vp],
+    "vggt_headnorm_rope_bwd": [_vp, _i64, _vp, _i64, _i, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _i, _vp, _vp, _i, _vp,
+                               _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp],
+    "vggt_colsum": [_vp, _i, _i64, _i, _i, _vp, _i, _vp, ctypes.c_size_t, _vp],
+    "vggt_layerscale_bwd": [_vp, _i64, _vp, _i, _i64, _vp, _vp, _i, _i64, _i, _i, _vp, _vp, _vp, ctypes.c_size_t,
+                            _vp],
+    "vggt_gelu_fwd": [_vp, _i, _i64, _vp, _i, _i64, _i, _i, _vp],
+    "vggt_gelu_bwd": [_vp, _i, _i64, _vp, _i, _i64, _vp, _i, _i64, _i, _i, _vp, _vp, ctypes.c_size_t, _vp],
+    "vggt_resid_scale_add": [_vp, _i64, _vp, _i, _i64, _vp, _i, _i, _vp],
+    "vggt_transpose_b16": [_vp, _i64, _i, _i, _vp, _i64, _i, _vp],
+    "vggt_wgrad_f32": [_vp, _i64, _vp, _i64, _i, _i, _i, _vp, _i64, _i, _vp],
+    "vggt_batch_dot_f32": [_vp, _vp, _i64, _i, _i64, _vp, _vp, ctypes.c_size_t, _vp],
 }
+_WS_FNS = {"vggt_colred_workspace_bytes": [_i, _i], "vggt_layernorm_bwd_workspace_bytes": [_i, _i],
+           "vggt_headnorm_rope_bwd_workspace_bytes": [_i, _i], "vggt_batch_dot_workspace_bytes": [_i, _i64]}
 
 _lib = None
 
@@ -82,6 +104,10 @@ def lib() -> ctypes.CDLL:
         L.vggt_version.restype = ctypes.c_char_p
         L.vggt_irls_workspace_bytes.argtypes = [_i]
         L.vggt_irls_workspace_bytes.restype = ctypes.c_size_t
+        for name, argt in _WS_FNS.items():
+            fn = getattr(L, name)
+            fn.argtypes = argt
+            fn.restype = ctypes.c_size_t
         _lib = L
     return _lib
 
@@ -419,3 +445,157 @@ def scale_(x: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
     rc = lib().vggt_scale_f32(_p(x), _bstride(x, n), B, n, _p(scale), _stream())
     _check(rc, "vggt_scale_f32")
     return x
+
+
+# ---------------------------------------------------------------- training (backward) wrappers
+_TRAIN_WS = {}
+
+
+def _train_ws(device, nbytes: int) -> torch.Tensor:
+    """Grow-only per-device scratch for the deterministic reduction partials
+    (stream-ordered reuse: every user consumes it before the next launch)."""
+    t = _TRAIN_WS.get(device)
+    if t is None or t.numel() * 4 < nbytes:
+        t = torch.empty((nbytes + 3) // 4 + 64, device=device, dtype=torch.float32)
+        _TRAIN_WS[device] = t
+    return t
+
+
+def attention_fwd_lse(q, k, v, o, lse: torch.Tensor, batch: int, heads: int, nq: int, nk: int, D: int,
+                      q_bstride: int, k_bstride: int, o_bstride: int, scale: Optional[float] = None) -> None:
+    _dev(q, "attention_fwd_lse")
+    assert lse.dtype == torch.float32 and lse.numel() >= batch * heads * nq
+    sc = D ** -0.5 if scale is None else scale
+    rc = lib().vggt_attention_fwd_lse(_p(q), _ld(q), q_bstride, _p(k), _ld(k), k_bstride, _p(v), _ld(v), k_bstride,
+                                      _p(o), _ld(o), o_bstride, _p(lse), batch, heads, nq, nk, D, float(sc), _stream())
+    _check(rc, "vggt_attention_fwd_lse")
+
+
+def attention_bwd(q, k, v, o, do, lse, dq, dk, dv, batch: int, heads: int, nq: int, nk: int, D: int, q_bstride: int,
+                  k_bstride: int, o_bstride: int, scale: Optional[float] = None) -> None:
+    """q/k/v/o/do/dq/dk/dv: 2-D bf16 row views; dk and dv share one leading dimension."""
+    _dev(q, "attention_bwd")
+    assert _ld(dk) == _ld(dv)
+    sc = D ** -0.5 if scale is None else scale
+    delta = _train_ws(q.device, 4 * batch * heads * nq)
+    rc = lib().vggt_attention_bwd(_p(q), _ld(q), q_bstride, _p(k), _ld(k), k_bstride, _p(v), _ld(v), _p(o), _p(do),
+                                  _ld(o), o_bstride, _p(lse), _p(delta), _p(dq), _ld(dq), _p(dk), _p(dv), _ld(dk),
+                                  batch, heads, nq, nk, D, float(sc), _stream())
+    _check(rc, "vggt_attention_bwd")
+
+
+def attention_small_bwd(q, k, v, do, dq, dk, dv, batch: int, heads: int, nq: int, nk: int, D: int, q_bstride: int,
+                        k_bstride: int, o_bstride: int, dq_bstride: int, dkv_bstride: int,
+                        scale: Optional[float] = None) -> None:
+    _dev(q, "attention_small_bwd")
+    assert _ld(dk) == _ld(dv) and _ld(do) is not None
+    sc = D ** -0.5 if scale is None else scale
+    rc = lib().vggt_attention_small_bwd(_p(q), _ld(q), q_bstride, _p(k), _ld(k), k_bstride, _p(v), _ld(v), _p(do),
+                                        _ld(do), o_bstride, _p(dq), _ld(dq), dq_bstride, _p(dk), _p(dv), _ld(dk),
+                                        dkv_bstride, _dt(q), batch, heads, nq, nk, D, float(sc), _stream())
+    _check(rc, "vggt_attention_small_bwd")
+
+
+def layernorm_bwd(x, w, eps: float, dy, dx, accumulate: bool, dw=None, db=None, M: Optional[int] = None,
+                  group: Optional[int] = None, x_gstride: int = 0, x_off: int = 0, y_gstride: int = 0,
+                  y_off: int = 0) -> None:
+    """dx (+)= LayerNorm backward; dw/db (+)= parameter gradients.  Identity
+    row map unless group/strides are given (vggt_layernorm_grouped's)."""
+    _dev(x, "layernorm_bwd")
+    M = x.shape[0] if M is None else M
+    C = x.shape[1]
+    L = lib()
+    nb = int(L.vggt_layernorm_bwd_workspace_bytes(M, C))
+    ws = _train_ws(x.device, nb)
+    g = (M if M > 0 else 1) if group is None else group
+    rc = L.vggt_layernorm_bwd(_p(x), _dt(x), _ld(x), _p(w), float(eps), _p(dy), _dt(dy), _ld(dy), _p(dx), _dt(dx),
+                              _ld(dx), int(accumulate), M, C, g, x_gstride, x_off, y_gstride, y_off, _p(dw), _p(db),
+                              _p(ws), ws.numel() * 4, _stream())
+    _check(rc, "vggt_layernorm_bwd")
+
+
+def headnorm_rope_bwd(pre, grad, H: int, hsplit: int, D: int, w0, w1, eps: float, mode: int, pos, period: int, cos,
+                      sin, dw0=None, db0=None, dw1=None, db1=None) -> None:
+    """In place grad := d(pre) for per-head LayerNorm + RoPE (pre / grad: 2-D row
+    views whose column 0 is head 0)."""
+    _dev(pre, "headnorm_rope_bwd")
+    M = pre.shape[0]
+    L = lib()
+    ws = _train_ws(pre.device, int(L.vggt_headnorm_rope_bwd_workspace_bytes(M, D)))
+    tab = cos.shape[0] if cos is not None else 0
+    rc = L.vggt_headnorm_rope_bwd(_p(pre), _ld(pre), _p(grad), _ld(grad), _dt(pre), M, H, hsplit, D, _p(w0), _p(w1),
+                                  float(eps), mode, _p(pos), period, _p(cos), _p(sin), tab, _p(dw0), _p(db0), _p(dw1),
+                                  _p(db1), _p(ws), ws.numel() * 4, _stream())
+    _check(rc, "vggt_headnorm_rope_bwd")
+
+
+def colsum(x, out, accumulate: bool = True) -> None:
+    _dev(x, "colsum")
+    M, N_ = x.shape
+    L = lib()
+    ws = _train_ws(x.device, int(L.vggt_colred_workspace_bytes(M, N_)))
+    _check(L.vggt_colsum(_p(x), _dt(x), _ld(x), M, N_, _p(out), int(accumulate), _p(ws), ws.numel() * 4, _stream()),
+           "vggt_colsum")
+
+
+def layerscale_bwd(dout, branch, gamma, dbranch, dgamma=None, dbias=None) -> None:
+    _dev(dout, "layerscale_bwd")
+    M, N_ = dout.shape
+    L = lib()
+    ws = _train_ws(dout.device, int(L.vggt_colred_workspace_bytes(M, N_)))
+    rc = L.vggt_layerscale_bwd(_p(dout), _ld(dout), _p(branch), _dt(branch), _ld(branch), _p(gamma), _p(dbranch),
+                               _dt(dbranch), _ld(dbranch), M, N_, _p(dgamma), _p(dbias), _p(ws), ws.numel() * 4,
+                               _stream())
+    _check(rc, "vggt_layerscale_bwd")
+
+
+def gelu_fwd(x, y) -> None:
+    _dev(x, "gelu_fwd")
+    M, N_ = x.shape
+    _check(lib().vggt_gelu_fwd(_p(x), _dt(x), _ld(x), _p(y), _dt(y), _ld(y), M, N_, _stream()), "vggt_gelu_fwd")
+
+
+def gelu_bwd(dh, pre, dpre, dbias=None) -> None:
+    _dev(dh, "gelu_bwd")
+    M, N_ = dh.shape
+    L = lib()
+    ws = _train_ws(dh.device, int(L.vggt_colred_workspace_bytes(M, N_)))
+    rc = L.vggt_gelu_bwd(_p(dh), _dt(dh), _ld(dh), _p(pre), _dt(pre), _ld(pre), _p(dpre), _dt(dpre), _ld(dpre), M, N_,
+                         _p(dbias), _p(ws), ws.numel() * 4, _stream())
+    _check(rc, "vggt_gelu_bwd")
+
+
+def resid_scale_add(x, branch, gamma) -> None:
+    _dev(x, "resid_scale_add")
+    M, N_ = x.shape
+    rc = lib().vggt_resid_scale_add(_p(x), _ld(x), _p(branch), _dt(branch), _ld(branch), _p(gamma), M, N_, _stream())
+    _check(rc, "vggt_resid_scale_add")
+
+
+def transpose_b16(src, dst, rows_pad: int) -> None:
+    """dst[c, r] = src[r, c]; dst columns [rows, rows_pad) zero."""
+    _dev(src, "transpose_b16")
+    rows, cols = src.shape
+    assert src.element_size() == 2 and dst.element_size() == 2 and dst.shape[0] >= cols and dst.shape[1] >= rows_pad
+    rc = lib().vggt_transpose_b16(_p(src), _ld(src), rows, cols, _p(dst), _ld(dst), rows_pad, _stream())
+    _check(rc, "vggt_transpose_b16")
+
+
+def wgrad_f32(dy, x, dw, accumulate: bool = True) -> None:
+    _dev(dy, "wgrad_f32")
+    M, N_ = dy.shape
+    K = x.shape[1]
+    assert x.shape[0] == M and dw.shape == (N_, K)
+    rc = lib().vggt_wgrad_f32(_p(dy), _ld(dy), _p(x), _ld(x), M, N_, K, _p(dw), _ld(dw), int(accumulate), _stream())
+    _check(rc, "vggt_wgrad_f32")
+
+
+def batch_dot_f32(a, c, out) -> None:
+    """out[b] = sum(a[b] * c[b]) (fp32, contiguous per-batch blocks)."""
+    _dev(a, "batch_dot_f32")
+    B = a.shape[0]
+    n = a[0].numel()
+    L = lib()
+    ws = _train_ws(a.device, int(L.vggt_batch_dot_workspace_bytes(B, n)))
+    rc = L.vggt_batch_dot_f32(_p(a), _p(c), _bstride(a, n), B, n, _p(out), _p(ws), ws.numel() * 4, _stream())
+    _check(rc, "vggt_batch_dot_f32")

@@ -30,6 +30,7 @@ from ..layers.cross_attention import CrossAttentionBlock
 from ..layers.gated_update import GatedUpdate
 from ..layers.rope import RotaryPositionEmbedding
 from ..runtime import Workspace, pack_linear, round_up
+from .. import autograd as AG
 
 logger = logging.getLogger(__name__)
 
@@ -117,11 +118,144 @@ class AlignmentHead(nn.Module):
         cos, sin = self.rope1d.tables(dim, int(pos.max()), device)
         return pos.to(torch.int32).to(device), cos, sin
 
-    @torch.no_grad()
+    def trainable(self) -> bool:
+        """Gradients requested for this head (training step, run_model.py:232)."""
+        return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+
     def forward(self, tokens: torch.Tensor, image_size: Tuple[int, int], next_num_overlap: int,
                 overlap_tokens: torch.Tensor = None, memory_tokens: torch.Tensor = None):
         """alignment_head.py:224-345 -> (chunk_sim3 (B,1,8), frame_se3 (B,S-1,7),
-        memory (B,N,dec)|None, new_overlap_tokens (B, ov+1, P+1, C))."""
+        memory (B,N,dec)|None, new_overlap_tokens (B, ov+1, P+1, C)).
+
+        With gradients enabled and trainable parameters this runs the
+        autograd path (aligned_vggt.autograd: checkpoint-style block Functions
+        with HIP backward kernels); otherwise the fused inference path."""
+        if self.trainable():
+            return self._forward_train(tokens, image_size, next_num_overlap, overlap_tokens, memory_tokens)
+        with torch.no_grad():
+            return self._forward_infer(tokens, image_size, next_num_overlap, overlap_tokens, memory_tokens)
+
+    def _positions(self, S: int, T: Optional[int], dev):
+        """Temporal 1-D RoPE positions (alignment_head.py:274-286): queries
+        att_ids, keys cross_ids (previous chunk's first frame at 0)."""
+        C = self.embed_dim
+        seq = torch.arange(S)
+        if T is not None:
+            att = seq + (S - (T - 1))
+            cross = torch.cat([seq[:1], seq[-(T - 1):]])
+            return self._rope1d(att, C // self.num_heads, dev), self._rope1d(cross, C // self.num_heads, dev)
+        r = self._rope1d(seq, C // self.num_heads, dev)
+        return r, r
+
+    def _forward_train(self, tokens, image_size, next_num_overlap, overlap_tokens, memory_tokens):
+        if tokens.device.type != "cuda":
+            raise RuntimeError("AlignmentHead: the MI355X hot path runs on HIP devices only (no CPU fallback)")
+        if not self.temporal_attention:
+            raise NotImplementedError("temporal_attention=False is not supported (see forward)")
+        if tokens.requires_grad:
+            raise NotImplementedError("gradients into the aggregator tokens: the reference training config freezes "
+                                      "the aggregator (train_featureAlignedVGGT_vkitti.yaml:80-83)")
+        H_img, W_img = image_size
+        B, S, P, Cin = tokens.shape
+        C = self.embed_dim
+        dev = tokens.device
+        P1 = P + 1
+        M = B * S * P1
+        x = AG.ProjectInFn.apply(tokens.detach().float().contiguous(), self, round_up(M, 256),
+                                 self.project_in.weight, self.project_in.bias, self.token_norm.weight,
+                                 self.token_norm.bias, self.per_frame_alignment_token)
+        first_chunk = overlap_tokens is None
+        if not first_chunk:
+            assert overlap_tokens.shape[0] == B and overlap_tokens.shape[2] == 1 + P and \
+                overlap_tokens.shape[3] == C, "Size of tokens and overlap tokens must match"
+            if overlap_tokens.device != dev:
+                raise RuntimeError("overlap_tokens must already be on the chunk's device "
+                                   "(the reference's .to() at alignment_head.py:256-257 is a no-op)")
+            T = overlap_tokens.shape[1]
+            # detached, alignment_head.py:262
+            y = overlap_tokens.detach().reshape(B * T * P1, C).float().contiguous()
+            nk = T
+        else:
+            T, y, nk = None, None, S
+        rq, rk = self._positions(S, T, dev)
+        r2 = self._rope2d(H_img // self.patch_size, W_img // self.patch_size, dev)
+        for i in range(self.aa_block_num):
+            fb = self.frame_blocks[i]
+            x = AG.FrameBlockFn.apply(x, fb, (B * S, P1), r2, *AG.frame_block_params(fb))
+            tb = self.temporal_blocks[i]
+            x = AG.TemporalBlockFn.apply(x, y, tb, B * P1, S, nk, rq, rk, *AG.temporal_block_params(tb))
+        tok4 = x.view(B, S, P1, C)
+        chunk_sim3, frame_se3, memory = self._decode_train(tok4[..., 0, :], next_num_overlap, first_chunk,
+                                                           memory_tokens)
+        new_overlap = torch.cat([tok4[:, :1], tok4[:, -next_num_overlap:]], dim=1).contiguous()
+        return chunk_sim3, frame_se3, memory, new_overlap
+
+    def _frame_dropout(self, frame_tokens: torch.Tensor, num_overlap: int, is_first_chunk: bool) -> torch.Tensor:
+        """alignment_head.py:500-510: training-mode dropout of non-overlap frame
+        tokens (not for the first chunk, never the overlap frames)."""
+        B, S1, _ = frame_tokens.shape
+        if self.training and self.drop_prob_nonoverlap > 0.0 and not is_first_chunk and (S1 - num_overlap) > 1:
+            keep = self._dropout_mask(B, S1 - num_overlap, frame_tokens.device)
+            mask = torch.cat((keep, torch.ones((B, num_overlap, 1), device=frame_tokens.device)), dim=1)
+            return frame_tokens * mask * (1.0 / (1.0 - self.drop_prob_nonoverlap))
+        return frame_tokens
+
+    def _dropout_mask(self, B: int, n: int, device) -> torch.Tensor:
+        return (torch.rand(B, n, device=device) > self.drop_prob_nonoverlap).float().unsqueeze(-1)
+
+    def _decode_train(self, frame_alignment_tokens, num_overlap, is_first_chunk, memory_tokens=None):
+        """_decode_alignments (alignment_head.py:427-540) on fp32 HIP autograd
+        Functions; memory tokens keep their gradient (:482-484)."""
+        B, S, Ce = frame_alignment_tokens.shape
+        dev = frame_alignment_tokens.device
+        dec = self.project_dec.out_features
+        nm = self.num_memory_tokens
+        seq = torch.arange(1, S)
+        cross = torch.arange(0, S + nm) if nm > 0 else torch.arange(0, S)
+        if nm > 0:
+            cross[-nm:] += S
+        hd = dec // self.num_heads
+        maxp = int(max(cross.max(), seq.max() if S > 1 else 0))
+        tabs = self.rope1d.tables(hd, maxp, dev)
+        i32 = lambda t: t.to(torch.int32).to(dev)
+        tok = AG.linear_f32(self.project_dec, frame_alignment_tokens.float())
+        tok = AG.layernorm_f32(self.dec_norm, tok)
+        directional = None
+        if nm > 0:
+            norm_t = tok.norm(dim=-1).mean(dim=-1, keepdim=True).unsqueeze(1)
+            if memory_tokens is None:
+                mem = self.memory_token.expand(B, *self.memory_token.shape[1:])
+                fi = AG.linear_f32(self.frame_proj, tok[:, 0]).view(B, nm, dec)
+                fdir = fi / fi.norm(dim=-1, keepdim=True).clamp_min(1e-6)
+                a = torch.sigmoid(self.alpha)
+                directional = (1 - a) * mem + a * fdir
+                eff = mem * norm_t
+            else:
+                directional = memory_tokens
+                eff = memory_tokens * norm_t
+            cross_tok = torch.cat([tok, eff], dim=1)
+        else:
+            cross_tok = tok
+        first = tok[:, :1]
+        pq, pk = i32(torch.zeros(1, dtype=cross.dtype)), i32(cross)
+        for blk in self.chunk_cross_blocks:
+            first = blk.forward_f32_train(first, cross_tok, pq, pk, tabs)
+        memory = self.gated_update.forward_train(directional, first) if nm > 0 else None
+        chunk_tok = AG.layernorm_f32(self.chunk_norm, first)
+        frame_tokens = self._frame_dropout(tok[:, 1:], num_overlap, is_first_chunk)
+        fq, fk = i32(seq), i32(torch.zeros(1, dtype=seq.dtype))
+        for blk in self.frame_cross_blocks:
+            frame_tokens = blk.forward_f32_train(frame_tokens, chunk_tok, fq, fk, tabs)
+        frame_tokens = AG.layernorm_f32(self.frame_norm, frame_tokens)
+        d = self.frame_se3_decoder
+        frame_se3 = AG.linear_f32(d.fc2, AG.linear_f32(d.fc1, frame_tokens, gelu=True))
+        d = self.chunk_sim3_decoder
+        cs = AG.linear_f32(d.fc2, AG.linear_f32(d.fc1, chunk_tok, gelu=True))
+        chunk_sim3 = torch.cat([cs[..., :-1], torch.exp(cs[..., -1:])], dim=-1)
+        return chunk_sim3, frame_se3, memory
+
+    def _forward_infer(self, tokens: torch.Tensor, image_size: Tuple[int, int], next_num_overlap: int,
+                       overlap_tokens: torch.Tensor = None, memory_tokens: torch.Tensor = None):
         if tokens.device.type != "cuda":
             raise RuntimeError("AlignmentHead: the MI355X hot path runs on HIP devices only (no CPU fallback)")
         if not self.temporal_attention:
@@ -187,7 +321,7 @@ class AlignmentHead(nn.Module):
     @torch.no_grad()
     def _decode_alignments(self, frame_alignment_tokens: torch.Tensor, num_overlap: int, is_first_chunk: bool,
                            memory_tokens: torch.Tensor = None):
-        """alignment_head.py:427-540 (fp32; eval mode -> no frame dropout)."""
+        """alignment_head.py:427-540 (fp32; frame dropout in training mode)."""
         B, S, Ce = frame_alignment_tokens.shape
         dev = frame_alignment_tokens.device
         dec = self.project_dec.out_features
@@ -234,7 +368,7 @@ class AlignmentHead(nn.Module):
         N.layernorm(first.reshape(B, dec), self.chunk_norm.weight, self.chunk_norm.bias, self.chunk_norm.eps,
                     chunk_tok)
         chunk_tok = chunk_tok.view(B, 1, dec)
-        frame_tokens = tok[:, 1:]
+        frame_tokens = self._frame_dropout(tok[:, 1:], num_overlap, is_first_chunk)
         for blk in self.frame_cross_blocks:
             frame_tokens = blk.forward_f32(frame_tokens, chunk_tok, i32(pos_frame_q), i32(pos_frame_k), tabs)
         fr = frame_tokens.reshape(B * (S - 1), dec)

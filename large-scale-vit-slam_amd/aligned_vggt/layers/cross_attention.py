@@ -23,6 +23,7 @@ import torch.nn as nn
 from .. import _native as N
 from ..backbone.layers import Attention, LayerScale, Mlp
 from ..runtime import Workspace, pack_linear
+from .. import autograd as AG
 
 
 class CrossAttention(nn.Module):
@@ -175,6 +176,34 @@ class CrossAttentionBlock(nn.Module):
         N.linear_f32(hid, self.mlp.fc2.weight, self.mlp.fc2.bias, xs, N.EPI_RESID_F32,
                      gamma=self._gamma(self.ls2, C, dev))
         return xs.view(B, Nq, C)
+
+
+    def forward_f32_train(self, x: torch.Tensor, y: torch.Tensor, pos_q: torch.Tensor, pos_k: torch.Tensor,
+                          rope_tabs) -> torch.Tensor:
+        """forward_f32 as fp32 HIP autograd Functions (decoder blocks under
+        training, alignment_head.py:487-526): x (B, Nq, C), y (B, Nk, C)."""
+        B, Nq, C = x.shape
+        Nk = y.shape[1]
+        H = self.attn.num_heads
+        D = C // H
+        a = self.attn
+        xn = AG.layernorm_f32(self.norm1, x)
+        yn = AG.layernorm_f32(self.norm3, y)
+        q = AG.linear_f32(a.q, xn).reshape(B * Nq, C)
+        k = AG.linear_f32(a.k, yn).reshape(B * Nk, C)
+        v = AG.linear_f32(a.v, yn).reshape(B * Nk, C)
+        mode = N.ROPE_1D if a.rope is not None else N.ROPE_NONE
+        qn, kn = a.q_norm, a.k_norm
+        if isinstance(qn, nn.LayerNorm) or mode != N.ROPE_NONE:
+            hn = isinstance(qn, nn.LayerNorm)
+            q = AG.HeadNormRopeF32Fn.apply(q, qn.weight if hn else None, qn.bias if hn else None,
+                                           qn.eps if hn else 0.0, H, D, mode, pos_q, rope_tabs)
+            k = AG.HeadNormRopeF32Fn.apply(k, kn.weight if hn else None, kn.bias if hn else None,
+                                           kn.eps if hn else 0.0, H, D, mode, pos_k, rope_tabs)
+        o = AG.AttnSmallF32Fn.apply(q, k, v, B, H, Nq, Nk, D)
+        x = x + self.ls1.gamma * AG.linear_f32(a.proj, o).view(B, Nq, C)
+        h = AG.linear_f32(self.mlp.fc1, AG.layernorm_f32(self.norm2, x), gelu=True)
+        return x + self.ls2.gamma * AG.linear_f32(self.mlp.fc2, h)
 
 
 class DecoderBlock(nn.Module):

@@ -13,6 +13,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _native as N
+from .. import autograd as AG
 
 
 class GatedUpdate(nn.Module):
@@ -51,6 +52,26 @@ class GatedUpdate(nn.Module):
         gl = torch.empty(B * Nt, 1, device=memory.device)
         N.linear_f32(gh, self.gate_mlp[2].weight, self.gate_mlp[2].bias, gl, N.EPI_F32)
         gate = torch.sigmoid(gl).view(B, Nt, 1)
+        orth = diff - (diff * memory).sum(-1, keepdim=True) * memory
+        d = F.normalize(orth, dim=-1)
+        return F.normalize(memory + gate * d, dim=-1)
+
+    def forward_train(self, memory: torch.Tensor, update: torch.Tensor) -> torch.Tensor:
+        """gated_update.py:43-79 on fp32 HIP autograd linears (training; the
+        gate input is detached as in the reference, :69)."""
+        B, Nt, D = memory.shape
+        assert Nt == self.num_tokens and D == self.token_dim
+        memory = memory.float()
+        scale = update.norm(dim=-1, keepdim=True)
+        upd = update.expand_as(memory)
+        mean_scaled = memory.mean(dim=1, keepdim=True).expand_as(memory) * scale
+        mem_scaled = memory * scale
+        inp = torch.cat([upd, mem_scaled, mean_scaled], dim=-1)
+        deltas = torch.stack([AG.linear_f32(mlp[2], AG.linear_f32(mlp[0], inp[:, i], gelu=True))
+                              for i, mlp in enumerate(self.delta_mlps)], dim=1)
+        diff = deltas - memory
+        g_in = torch.cat([diff, mem_scaled], dim=-1).detach()
+        gate = torch.sigmoid(AG.linear_f32(self.gate_mlp[2], AG.linear_f32(self.gate_mlp[0], g_in, gelu=True)))
         orth = diff - (diff * memory).sum(-1, keepdim=True) * memory
         d = F.normalize(orth, dim=-1)
         return F.normalize(memory + gate * d, dim=-1)

@@ -15,6 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _native as N
+from .. import autograd as AG
 from ..backbone.aggregator import Aggregator
 from ..backbone.camera_head import CameraHead
 from ..backbone.dpt_head import DPTHead
@@ -63,15 +64,31 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
                                             num_memory_tokens=cfg.num_memory_tokens,
                                             temporal_attention=cfg.temporal_attention).to(dev)
 
-    @torch.no_grad()
     def forward(self, images: torch.Tensor, num_overlap: int, context: dict = None, gt_poses: torch.Tensor = None) -> dict:
         """featureAligned_vggt.py:48-225.  Split into the context-free
         :meth:`encode_chunk` (aggregator + camera/depth/point heads: ~99% of
         the FLOPs, embarrassingly parallel over chunks) and the recurrent
         :meth:`align_chunk` (alignment head + Sim(3)/SE(3) composition), so the
         multi-GPU pipeline (aligned_vggt.dist) can run encodes ahead of the
-        alignment baton.  forward == align_chunk(encode_chunk(.)) exactly."""
+        alignment baton.  forward == align_chunk(encode_chunk(.)) exactly.
+
+        Training (gradients enabled and trainable alignment-head parameters,
+        run_model.py:232-249): the frozen encoders run without autograd, the
+        alignment head and the pose / depth composition carry gradients --
+        into the chunk's own outputs and, through the memory tokens and the
+        context's last pose encoding, into the previous chunks."""
+        if self.alignment_head.trainable():
+            self._check_frozen()
         return self.align_chunk(self.encode_chunk(images), num_overlap, context, gt_poses)
+
+    def _check_frozen(self) -> None:
+        for name in ("aggregator", "camera_head", "depth_head", "point_head", "track_head"):
+            m = getattr(self, name, None)
+            if m is not None and any(p.requires_grad for p in m.parameters()):
+                raise NotImplementedError(
+                    f"training {name}: only the alignment head is trainable on the MI355X path; freeze "
+                    f"'*aggregator*', '*camera_head*', '*depth_head*' as train_featureAlignedVGGT_vkitti.yaml:80-83 "
+                    f"does (requires_grad=False)")
 
     @torch.no_grad()
     def encode_chunk(self, images: torch.Tensor) -> dict:
@@ -86,8 +103,12 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
             enc["points"], enc["points_conf"] = self.point_head(toks, images=images, patch_start_idx=patch_start_idx)
         return enc
 
-    @torch.no_grad()
     def align_chunk(self, enc: dict, num_overlap: int, context: dict = None, gt_poses: torch.Tensor = None) -> dict:
+        train = self.alignment_head.trainable()
+        with torch.set_grad_enabled(train):
+            return self._align_chunk(enc, num_overlap, context, gt_poses, train)
+
+    def _align_chunk(self, enc: dict, num_overlap: int, context, gt_poses, train: bool) -> dict:
         images = enc["images"]
         toks = enc["tokens"]
         B, S, C, H, W = images.shape
@@ -153,7 +174,10 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
                     predictions["memory_tokens"] = context["memory_tokens"]
 
         if self.depth_head is not None:
-            depth = N.scale_(enc["depth"], chunk_scale.reshape(B))  # in place, featureAligned_vggt.py:171
+            if train:  # d chunk_scale = sum(d depth * depth_raw)
+                depth = AG.ScaleFn.apply(enc["depth"], chunk_scale.reshape(B))
+            else:
+                depth = N.scale_(enc["depth"], chunk_scale.reshape(B))  # in place, featureAligned_vggt.py:171
             depth_conf = enc["depth_conf"]
             if context is None:
                 predictions["depth"] = [depth]
@@ -172,8 +196,12 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
                     pt = pt @ point_identity_alignment.view(B, 1, 4, 4)
                 else:
                     pt = point_identity_alignment.view(B, 1, 4, 4)
-                # featureAligned_vggt.py:200-206: scale, then the SE(3) of pt, one HIP pass
-                pts3d = N.sim3_points(pts3d.contiguous(), pt[:, 0], chunk_scale.reshape(B))
+                if train:  # differentiable form (gradients into chunk_scale and pt)
+                    pts3d = pts3d * chunk_scale.view(B, 1, 1, 1, 1)
+                    pts3d = torch.einsum("bij,bshwj->bshwi", pt[:, 0, :3, :3], pts3d) + pt[:, 0, :3, 3].view(B, 1, 1, 1, 3)
+                else:
+                    # featureAligned_vggt.py:200-206: scale, then the SE(3) of pt, one HIP pass
+                    pts3d = N.sim3_points(pts3d.contiguous(), pt[:, 0], chunk_scale.reshape(B))
             if context is None:
                 predictions["world_points"] = [pts3d]
                 predictions["world_points_conf"] = [pts3d_conf]

@@ -50,7 +50,8 @@ struct AttnArgs {
   int64_t ldq, ldk, ldv, ldo;
   int64_t qbs, kbs, vbs, obs;
   int batch, heads, nq, nk;
-  float c;  // scale * log2(e)
+  float c;     // scale * log2(e)
+  float* lse;  // optional [batch*heads*nq]: log2 sum exp2(scores * c) per row (training recompute)
 };
 
 // LDS-DMA: 16 B per lane from buffer `rsrc` at per-lane byte offset `voff`
@@ -501,6 +502,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
     l_run = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
   }
   const float inv = 1.f / l_run;
+  if (a.lse && hl == 0 && qrow < a.nq) a.lse[((int64_t)b * a.heads + h) * a.nq + qrow] = m_run + __log2f(l_run);
   if (qrow < a.nq) {
     bf16_t* op = a.o + ((int64_t)b * a.obs + qrow) * a.ldo + h * D;
 #pragma unroll
@@ -529,7 +531,7 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
   if ((uint64_t)BKV * (uint64_t)(ldk > ldv ? ldk : ldv) * 2 >= (1ull << 31)) return VGGT_ERR_SHAPE;
   AttnArgs a{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, ldq, ldk, ldv, ldo,
              q_bstride, k_bstride, v_bstride, o_bstride, batch, heads, nq, nk,
-             scale * 1.4426950408889634f};
+             scale * 1.4426950408889634f, nullptr};
   // 8-wave workgroups (256 query rows) for long sequences; 4-wave ones
   // (128 rows) when the query count is short enough that the padding of a
   // 256-row block would cost more than the pairing gains.
@@ -576,6 +578,30 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
 #undef VGGT_ATTN_CASE
     default: return VGGT_ERR_UNSUPPORTED;
   }
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+// Training recompute (alignment-head frame blocks under checkpoint, SURVEY §8f
+// row 4): the exact-score offset-free form (variant 96: no Q prescale, so the
+// backward's recomputed scores match bit for bit) that also stores the per-row
+// log2-sum-exp consumed by vggt_attention_bwd.
+extern "C" int vggt_attention_fwd_lse(const void* q, int64_t ldq, int64_t q_bstride, const void* k, int64_t ldk,
+                                      int64_t k_bstride, const void* v, int64_t ldv, int64_t v_bstride, void* o,
+                                      int64_t ldo, int64_t o_bstride, float* lse, int batch, int heads, int nq, int nk,
+                                      int D, float scale, void* stream) {
+  if (batch <= 0 || heads <= 0 || nq <= 0 || nk <= 0 || !lse) return VGGT_ERR_SHAPE;
+  if (D != 64 && D != 128) return VGGT_ERR_UNSUPPORTED;
+  if ((ldq | ldk | ldv | ldo) % 8 || ((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) % 16)
+    return VGGT_ERR_ALIGN;
+  if ((uint64_t)BKV * (uint64_t)(ldk > ldv ? ldk : ldv) * 2 >= (1ull << 31)) return VGGT_ERR_SHAPE;
+  AttnArgs a{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, ldq, ldk, ldv, ldo,
+             q_bstride, k_bstride, v_bstride, o_bstride, batch, heads, nq, nk,
+             scale * 1.4426950408889634f, lse};
+  const int nwg = ((nq + 127) / 128) * heads * batch;
+  hipStream_t s = (hipStream_t)stream;
+  if (D == 64) attn_fwd_kernel<64, 4, 96><<<nwg, 256, 0, s>>>(a);
+  else attn_fwd_kernel<128, 4, 96><<<nwg, 256, 0, s>>>(a);
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
 }

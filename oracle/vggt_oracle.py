@@ -539,7 +539,7 @@ def gated_update(sd: SD, p: str, memory: Tensor, update: Tensor) -> Tensor:
         h = F.gelu(F.linear(inp[:, i], sd[f"{p}delta_mlps.{i}.0.weight"], sd[f"{p}delta_mlps.{i}.0.bias"]))
         deltas.append(F.linear(h, sd[f"{p}delta_mlps.{i}.2.weight"], sd[f"{p}delta_mlps.{i}.2.bias"]))
     diff = torch.stack(deltas, dim=1) - memory
-    g_in = torch.cat([diff, mem_scaled], dim=-1)
+    g_in = torch.cat([diff, mem_scaled], dim=-1).detach()  # gated_update.py:69: the gate sees no gradient path
     g = F.linear(F.gelu(F.linear(g_in, sd[p + "gate_mlp.0.weight"], sd[p + "gate_mlp.0.bias"])),
                  sd[p + "gate_mlp.2.weight"], sd[p + "gate_mlp.2.bias"])
     g = torch.sigmoid(g)
@@ -623,7 +623,8 @@ def alignment_head(sd: SD, tokens: Tensor, image_size, next_num_overlap: int, ov
         tokens = block(sd, f"{p}frame_blocks.{i}.", tokens.reshape(B * S, P, C), num_heads, pos2d, "2d", True, bf16=bf16)
         # alignment_head.py:372-380: a raw .view (not a permute) of (B,S,P,C) as (B*P,S,C)
         x = tokens.reshape(B * P, S, C)
-        y = overlap_tokens.reshape(B * P, T, C) if overlap_tokens is not None else x
+        # overlap tokens are detached (alignment_head.py:262): no gradient into the previous chunk
+        y = overlap_tokens.detach().reshape(B * P, T, C) if overlap_tokens is not None else x
         tokens = cross_attention_block(sd, f"{p}temporal_blocks.{i}.", x, y, num_heads, pos_t, bf16)
     tokens = tokens.reshape(B, S, P, C)
     chunk_sim3, frame_se3, mem = decode_alignments(sd, p, tokens[..., 0, :].float(), num_memory_tokens, memory_tokens)

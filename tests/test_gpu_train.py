@@ -1,0 +1,382 @@
+"""Alignment-head training on the HIP path: backward
+kernels through the C ABI against plain PyTorch fp32 autograd of the same op,
+block / head / full-model gradients against autograd of the CPU oracle
+(alignment_head.py, cross_attention.py, gated_update.py restated in
+oracle/vggt_oracle.py).
+
+Tolerances (relative L2, written per test): bf16 backward kernels vs fp32
+autograd on the same bf16-rounded inputs 2e-2 (P and dS are rounded to bf16
+for the matrix products, as flash-attention backward does); fp32 kernels
+1e-4; parameter gradients of the bf16-mixed trunk vs the oracle's bf16
+emulation: within 5e-2, or no further from the fp32 oracle than twice the
+oracle's own bf16-vs-fp32 spread (the same rule as the forward tests)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from oracle import vggt_oracle as O  # noqa: E402
+
+
+def _rel(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.fixture(scope="module")
+def N():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from aligned_vggt import _native
+    return _native
+
+
+def _bf(t):
+    return t.to(torch.bfloat16)
+
+
+# ------------------------------------------------------------------ attention (flash) backward
+@pytest.mark.parametrize("D,n,nb,H", [(128, 150, 2, 2), (64, 300, 1, 3), (128, 1375, 1, 1)])
+def test_attention_fwd_lse_and_bwd(N, D, n, nb, H):
+    torch.manual_seed(0)
+    C = H * D
+    qkv = _bf(torch.randn(nb * n, 3 * C, device="cuda"))
+    ao = torch.empty(nb * n, C, device="cuda", dtype=torch.bfloat16)
+    lse = torch.empty(nb * H * n, device="cuda")
+    N.attention_fwd_lse(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], ao, lse, nb, H, n, n, D, n, n, n)
+    do = _bf(torch.randn(nb * n, C, device="cuda"))
+    dqkv = torch.zeros(nb * n, 3 * C, device="cuda", dtype=torch.bfloat16)
+    N.attention_bwd(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], ao, do, lse, dqkv[:, :C], dqkv[:, C:2 * C],
+                    dqkv[:, 2 * C:], nb, H, n, n, D, n, n, n)
+    torch.cuda.synchronize()
+    # fp32 autograd reference on the same bf16 inputs
+    x = qkv.float().view(nb, n, 3, H, D).permute(2, 0, 3, 1, 4).contiguous().requires_grad_(True)
+    q, k, v = x[0], x[1], x[2]
+    s = (q @ k.transpose(-1, -2)) * D ** -0.5
+    o = torch.softmax(s, -1) @ v
+    o.backward(do.float().view(nb, n, H, D).transpose(1, 2))
+    ref_o = o.detach().transpose(1, 2).reshape(nb * n, C)
+    ref_lse = (torch.logsumexp(s.detach(), -1) * math.log2(math.e)).reshape(-1)
+    assert _rel(ao, ref_o) < 1e-2
+    assert (lse - ref_lse).abs().max().item() < 2e-3
+    g = x.grad.permute(1, 3, 0, 2, 4).reshape(nb * n, 3 * C)
+    for i, nm in enumerate(("dq", "dk", "dv")):
+        e = _rel(dqkv[:, i * C:(i + 1) * C], g[:, i * C:(i + 1) * C])
+        assert e < 2e-2, (nm, e)
+
+
+@pytest.mark.parametrize("dtype,groups,H,nq,nk,D", [(torch.bfloat16, 40, 2, 5, 3, 128),
+                                                    (torch.bfloat16, 30, 8, 6, 6, 128),
+                                                    (torch.float32, 2, 8, 1, 12, 64),
+                                                    (torch.float32, 3, 8, 15, 1, 64)])
+def test_attention_small_bwd(N, dtype, groups, H, nq, nk, D):
+    torch.manual_seed(1)
+    C = H * D
+    q = torch.randn(groups * nq, C, device="cuda").to(dtype)
+    kv = torch.randn(groups * nk, 2 * C, device="cuda").to(dtype)
+    do = torch.randn(groups * nq, C, device="cuda").to(dtype)
+    dq = torch.empty_like(q)
+    dkv = torch.empty_like(kv)
+    N.attention_small_bwd(q, kv[:, :C], kv[:, C:], do, dq, dkv[:, :C], dkv[:, C:], groups, H, nq, nk, D, nq, nk, nq,
+                          nq, nk)
+    torch.cuda.synchronize()
+    qq = q.float().view(groups, nq, H, D).transpose(1, 2).requires_grad_(True)
+    kk = kv[:, :C].float().reshape(groups, nk, H, D).transpose(1, 2).requires_grad_(True)
+    vv = kv[:, C:].float().reshape(groups, nk, H, D).transpose(1, 2).requires_grad_(True)
+    o = torch.softmax((qq @ kk.transpose(-1, -2)) * D ** -0.5, -1) @ vv
+    o.backward(do.float().view(groups, nq, H, D).transpose(1, 2))
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
+    assert _rel(dq, qq.grad.transpose(1, 2).reshape(-1, C)) < tol
+    assert _rel(dkv[:, :C], kk.grad.transpose(1, 2).reshape(-1, C)) < tol
+    assert _rel(dkv[:, C:], vv.grad.transpose(1, 2).reshape(-1, C)) < tol
+
+
+# ------------------------------------------------------------------ norms
+@pytest.mark.parametrize("C,xdt,dydt,acc", [(1024, torch.float32, torch.bfloat16, True),
+                                            (512, torch.float32, torch.float32, False),
+                                            (1024, torch.bfloat16, torch.float32, False)])
+def test_layernorm_bwd(N, C, xdt, dydt, acc):
+    torch.manual_seed(2)
+    M = 77
+    x = (torch.randn(M, C, device="cuda") * 3 + 1).to(xdt)
+    w = 1 + 0.1 * torch.randn(C, device="cuda")
+    b = 0.1 * torch.randn(C, device="cuda")
+    dy = torch.randn(M, C, device="cuda").to(dydt)
+    dx0 = torch.randn(M, C, device="cuda")
+    dx = dx0.clone() if acc else torch.empty(M, C, device="cuda", dtype=torch.float32)
+    dw, db = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+    N.layernorm_bwd(x, w, 1e-5, dy, dx, acc, dw, db)
+    torch.cuda.synchronize()
+    xr = x.float().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    F.layer_norm(xr, (C,), wr, br, 1e-5).backward(dy.float())
+    ref = xr.grad + (dx0 if acc else 0)
+    assert _rel(dx, ref) < 1e-5 and _rel(dw, wr.grad) < 1e-5 and _rel(db, br.grad) < 1e-5
+
+
+def test_layernorm_bwd_grouped(N):
+    """token_norm of the alignment head: input rows p of frame f, output rows f*(P+1)+1+p."""
+    torch.manual_seed(3)
+    F_, P, C = 5, 13, 1024
+    x = _bf(torch.randn(F_ * P, C, device="cuda"))
+    w, b = 1 + 0.1 * torch.randn(C, device="cuda"), 0.1 * torch.randn(C, device="cuda")
+    dyfull = torch.randn(F_ * (P + 1), C, device="cuda")
+    dx = torch.empty(F_ * P, C, device="cuda", dtype=torch.bfloat16)
+    dw, db = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+    N.layernorm_bwd(x, w, 1e-5, dyfull, dx, False, dw, db, M=F_ * P, group=P, x_gstride=P, x_off=0,
+                    y_gstride=P + 1, y_off=1)
+    dy = dyfull.view(F_, P + 1, C)[:, 1:].reshape(F_ * P, C)
+    xr = x.float().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    F.layer_norm(xr, (C,), wr, br, 1e-5).backward(dy)
+    assert _rel(dx, xr.grad) < 5e-3 and _rel(dw, wr.grad) < 1e-5 and _rel(db, br.grad) < 1e-5
+
+
+@pytest.mark.parametrize("D,mode,dtype", [(128, 1, torch.bfloat16), (64, 1, torch.bfloat16), (128, 2, torch.bfloat16),
+                                          (64, 2, torch.float32), (64, 0, torch.float32)])
+def test_headnorm_rope_bwd(N, D, mode, dtype):
+    """q_norm/k_norm (+ RoPE-2D / 1-D) backward on a fused [q | k] row (hsplit)."""
+    torch.manual_seed(4)
+    H, M = 3, 40
+    C = H * D
+    pre = (torch.randn(M, 2 * C, device="cuda") * 2).to(dtype)
+    g = torch.randn(M, 2 * C, device="cuda").to(dtype)
+    wq, bq = 1 + 0.1 * torch.randn(D, device="cuda"), 0.1 * torch.randn(D, device="cuda")
+    wk, bk = 1 + 0.1 * torch.randn(D, device="cuda"), 0.1 * torch.randn(D, device="cuda")
+    period = 10
+    if mode == 1:
+        pos = torch.randint(0, 7, (period, 2), device="cuda", dtype=torch.int32)
+        rd = D // 2
+    elif mode == 2:
+        pos = torch.randint(0, 7, (period,), device="cuda", dtype=torch.int32)
+        rd = D
+    else:
+        pos, rd = None, D
+    cos, sin = O.rope_cos_sin(rd, 8, 100.0)
+    cos, sin = cos.cuda().contiguous(), sin.cuda().contiguous()
+    grad = g.clone()
+    dwq, dbq, dwk, dbk = (torch.zeros(D, device="cuda") for _ in range(4))
+    N.headnorm_rope_bwd(pre, grad, 2 * H, H, D, wq, wk, 1e-5, mode, pos, period, cos if mode else None,
+                        sin if mode else None, dwq, dbq, dwk, dbk)
+    torch.cuda.synchronize()
+    # fp32 autograd reference: per-head LayerNorm then RoPE (oracle restatement)
+    x = pre.float().view(M, 2, H, D).requires_grad_(True)
+    ws = [p.clone().requires_grad_(True) for p in (wq, bq, wk, bk)]
+    y = torch.stack([F.layer_norm(x[:, 0], (D,), ws[0], ws[1], 1e-5), F.layer_norm(x[:, 1], (D,), ws[2], ws[3], 1e-5)],
+                    1)
+    rows = torch.arange(M, device="cuda") % period
+    if mode == 1:
+        p = pos.long()[rows]
+        half = D // 2
+        c, s_ = cos.cpu(), sin.cpu()
+        yv, yh = y[..., :half], y[..., half:]
+
+        def rot(t, pp):
+            cc = c.cuda()[pp][:, None, None, :]
+            ss = s_.cuda()[pp][:, None, None, :]
+            return t * cc + O._rotate_half(t) * ss
+        y = torch.cat([rot(yv, p[:, 0]), rot(yh, p[:, 1])], -1)
+    elif mode == 2:
+        p = pos.long()[rows]
+        y = y * cos[p][:, None, None, :] + O._rotate_half(y) * sin[p][:, None, None, :]
+    y.backward(g.float().view(M, 2, H, D))
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    assert _rel(grad, x.grad.view(M, 2 * C)) < tol
+    for got, ref in zip((dwq, dbq, dwk, dbk), ws):
+        assert _rel(got, ref.grad) < (5e-3 if dtype == torch.bfloat16 else 1e-5)
+
+
+# ------------------------------------------------------------------ reductions / elementwise
+def test_colsum_layerscale_gelu_resid(N):
+    torch.manual_seed(5)
+    M, C = 301, 1024
+    a = torch.randn(M, C, device="cuda")
+    out = torch.zeros(C, device="cuda")
+    N.colsum(_bf(a), out)
+    assert _rel(out, _bf(a).float().sum(0)) < 1e-5
+    br = _bf(torch.randn(M, C, device="cuda"))
+    gam = 0.01 * torch.randn(C, device="cuda")
+    dbr = torch.empty(M, C, device="cuda", dtype=torch.bfloat16)
+    dg, dbias = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+    N.layerscale_bwd(a, br, gam, dbr, dg, dbias)
+    assert _rel(dbr, gam * a) < 5e-3
+    assert _rel(dg, (a * br.float()).sum(0)) < 1e-5
+    assert _rel(dbias, dbr.float().sum(0)) < 1e-5
+    pre = _bf(torch.randn(M, 4 * C // 4, device="cuda") * 2)
+    h = torch.empty_like(pre)
+    N.gelu_fwd(pre, h)
+    assert _rel(h, F.gelu(pre.float())) < 5e-3
+    dh = _bf(torch.randn_like(pre.float()))
+    dpre = torch.empty_like(pre)
+    db1 = torch.zeros(pre.shape[1], device="cuda")
+    N.gelu_bwd(dh, pre, dpre, db1)
+    x = pre.float().requires_grad_(True)
+    F.gelu(x).backward(dh.float())
+    assert _rel(dpre, x.grad) < 5e-3 and _rel(db1, dpre.float().sum(0)) < 1e-5
+    xr = torch.randn(M, C, device="cuda")
+    ref = xr + gam * br.float()
+    N.resid_scale_add(xr, br, gam)
+    assert _rel(xr, ref) < 1e-6
+
+
+def test_transpose_wgrad_batchdot(N):
+    torch.manual_seed(6)
+    src = _bf(torch.randn(70, 200, device="cuda"))
+    dst = torch.full((200, 128), 7.0, device="cuda").to(torch.bfloat16)
+    N.transpose_b16(src, dst, 128)
+    torch.cuda.synchronize()
+    assert torch.equal(dst[:, :70], src.t()) and bool((dst[:, 70:] == 0).all())
+    dy, x = torch.randn(9, 300, device="cuda"), torch.randn(9, 1536, device="cuda")
+    dw = torch.zeros(300, 1536, device="cuda")
+    N.wgrad_f32(dy, x, dw, True)
+    assert _rel(dw, dy.t() @ x) < 1e-5
+    a, c = torch.randn(3, 2, 50, 60, device="cuda"), torch.randn(3, 2, 50, 60, device="cuda")
+    out = torch.empty(3, device="cuda")
+    N.batch_dot_f32(a, c, out)
+    assert _rel(out, (a * c).sum((1, 2, 3))) < 1e-5
+
+
+def test_bf16_weight_grad_gemm(N):
+    """dW = dY^T X through transposes + the forward GEMM (zero-padded token dim)."""
+    from aligned_vggt.autograd import _LinBwd
+    from aligned_vggt.runtime import Workspace
+    torch.manual_seed(7)
+    M, Nn, K = 1000, 1024, 2048
+    dy, x = _bf(torch.randn(M, Nn, device="cuda")), _bf(torch.randn(M, K, device="cuda"))
+    out = torch.empty(Nn, K, device="cuda")
+    _LinBwd(Workspace.get(torch.device("cuda", torch.cuda.current_device())), M).dw(dy, x, out)
+    assert _rel(out, dy.float().t() @ x.float()) < 4e-3
+
+
+# ------------------------------------------------------------------ blocks / head vs oracle autograd
+def _head_and_sd(seed=11, nm=8):
+    from aligned_vggt.heads.alignment_head import AlignmentHead
+    from aligned_vggt.utils.synthetic import synthetic_init_
+    head = AlignmentHead(in_dim=2048, num_memory_tokens=nm)
+    synthetic_init_(head, seed=seed)
+    with torch.no_grad():  # well-conditioned pose decoders (utils.synthetic.condition_pose_outputs_)
+        for dec in (head.chunk_sim3_decoder, head.frame_se3_decoder):
+            dec.fc2.bias.zero_()
+            dec.fc2.bias[6] = 1.0
+    sd = {"alignment_head." + k: v.detach().clone() for k, v in head.state_dict().items()}
+    return head.cuda().train(), sd
+
+
+def _grad_compare(head, sd_bf, sd_32, report):
+    errs = {}
+    for name, p in head.named_parameters():
+        key = "alignment_head." + name
+        gr, g32 = sd_bf[key].grad, sd_32[key].grad
+        if gr is None or p.grad is None:
+            assert (p.grad is None or p.grad.abs().max() == 0) and (gr is None or gr.abs().max() == 0), name
+            continue
+        e, e32, eref = _rel(p.grad, gr), _rel(p.grad, g32), _rel(gr, g32)
+        errs[name] = (e, e32, eref)
+    bad = {k: v for k, v in errs.items() if not (v[0] < 5e-2 or v[1] < 2.0 * v[2])}
+    worst = sorted(errs.items(), key=lambda kv: -kv[1][0])[:8]
+    print(report, "worst (hip-vs-bf16emu, hip-vs-fp32, ref-bf16-vs-fp32):", worst)
+    assert not bad, bad
+    return errs
+
+
+@pytest.mark.parametrize("S,ov,h,w", [(4, 2, 3, 4), (5, 1, 2, 3)])
+def test_alignment_head_two_chunk_gradients(N, S, ov, h, w):
+    """Two chunks with memory recurrence (gradients flow through the memory
+    tokens into chunk 1; overlap tokens are detached, alignment_head.py:262)."""
+    head, sd = _head_and_sd()
+    head.drop_prob_nonoverlap = 0.0  # the oracle has no dropout mask (tested separately)
+    P = 5 + h * w
+    H_img, W_img = 14 * h, 14 * w
+    g = torch.Generator().manual_seed(21)
+    toks = [torch.randn(1, S, P, 2048, generator=g) for _ in range(2)]
+    wts = {k: torch.randn(*shp, generator=g) for k, shp in
+           (("cs", (1, 1, 8)), ("fs", (1, S - 1, 7)), ("mem", (1, 8, 512)), ("ov", (1, ov + 1, P + 1, 1024)))}
+
+    def loss_of(outs, dev):
+        (cs1, fs1, m1, o1), (cs2, fs2, m2, o2) = outs
+        W = {k: v.to(dev) for k, v in wts.items()}
+        return ((cs1 * W["cs"]).sum() + (fs1 * W["fs"]).sum() + (cs2 * W["cs"]).sum() + 2 * (fs2 * W["fs"]).sum()
+                + (m2 * W["mem"]).sum() + 1e-2 * (o2 * W["ov"]).sum())
+
+    o1 = head(toks[0].cuda(), (H_img, W_img), ov)
+    o2 = head(toks[1].cuda(), (H_img, W_img), ov, overlap_tokens=o1[3], memory_tokens=o1[2])
+    loss_of((o1, o2), "cuda").backward()
+    torch.cuda.synchronize()
+    refs = {}
+    for tag, bf in (("bf", True), ("32", False)):
+        sdr = {k: v.clone().requires_grad_(v.is_floating_point()) for k, v in sd.items()}
+        r1 = O.alignment_head(sdr, toks[0], (H_img, W_img), ov, None, None, bf16=bf)
+        r2 = O.alignment_head(sdr, toks[1], (H_img, W_img), ov, r1[3], r1[2], bf16=bf)
+        loss_of((r1, r2), "cpu").backward()
+        refs[tag] = (sdr, r1, r2)
+    for a, b in zip(o2, refs["bf"][2]):
+        assert _rel(a, b) < 3e-2
+    _grad_compare(head, refs["bf"][0], refs["32"][0], f"S={S} ov={ov}")
+
+
+def test_frame_dropout_mask(N):
+    """Training-mode frame dropout (alignment_head.py:500-510): non-overlap
+    frames of a non-first chunk are zeroed / rescaled by the same mask the
+    reference draws; overlap frames never."""
+    head, _ = _head_and_sd()
+    B, S1, ov = 2, 9, 3
+    t = torch.ones(B, S1, 4, device="cuda")
+    torch.manual_seed(0)
+    out = head._frame_dropout(t, ov, False)
+    torch.manual_seed(0)
+    keep = (torch.rand(B, S1 - ov, device="cuda") > head.drop_prob_nonoverlap).float()
+    ref = torch.cat([keep, torch.ones(B, ov, device="cuda")], 1)[..., None] / (1 - head.drop_prob_nonoverlap)
+    assert torch.equal(out, t * ref)
+    assert torch.equal(head._frame_dropout(t, ov, True), t)  # first chunk: none
+    head.eval()
+    assert torch.equal(head._frame_dropout(t, ov, False), t)
+
+
+def test_feature_aligned_training_step(N):
+    """FeatureAlignedVGGT in training mode with the reference's freeze list:
+    two chunks, gradients of a pose + depth + Sim(3) loss reach only the
+    alignment head and match autograd through the oracle's composition
+    (featureAligned_vggt.py:48-225) on the same tokens."""
+    from aligned_vggt.models.featureAligned_vggt import FeatureAlignedVGGT
+    from aligned_vggt.utils.synthetic import condition_pose_outputs_, synthetic_images, synthetic_init_
+    m = FeatureAlignedVGGT(enable_point=False, enable_track=False, num_memory_tokens=8)
+    synthetic_init_(m, seed=11)
+    condition_pose_outputs_(m)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.cuda().train()
+    m.alignment_head.drop_prob_nonoverlap = 0.0
+    for name, p in m.named_parameters():
+        p.requires_grad_(name.startswith("alignment_head."))
+    S, ov, H, W = 3, 1, 42, 56
+    imgs = synthetic_images(1, 2 * S - ov, H, W, seed=5)
+    chunks = O.generate_chunks(imgs.shape[1], S, ov)
+    ctx = None
+    for ids in chunks:
+        ctx = m(imgs[:, ids].cuda(), ov, ctx)
+    g = torch.Generator().manual_seed(3)
+    wp = torch.randn(1, S, 9, generator=g)
+    wd = torch.randn(1, S, H, W, 1, generator=g) / (H * W)
+    wc = torch.randn(1, len(chunks), 8, generator=g)
+
+    def loss_of(pred, dev):
+        l = sum((pe * wp.to(dev)).sum() for pe in pred["pose_enc"])
+        l = l + sum((d * wd.to(dev)).sum() for d in pred["depth"])
+        return l + (pred["chunk_sim3_alignment_enc"] * wc.to(dev)).sum()
+
+    loss_of(ctx, "cuda").backward()
+    torch.cuda.synchronize()
+    assert all(p.grad is None for n, p in m.named_parameters() if not n.startswith("alignment_head."))
+    assert all(torch.isfinite(p.grad).all() for n, p in m.named_parameters() if p.grad is not None)
+    refs = {}
+    for tag, bf in (("bf", True), ("32", False)):
+        sdr = {k: (v.clone().requires_grad_(True) if k.startswith("alignment_head.") and v.is_floating_point()
+                   else v) for k, v in sd.items()}
+        rc = None
+        for ids in chunks:
+            rc = O.feature_aligned_forward(sdr, imgs[:, ids], ov, rc, bf16=bf, training=True)
+        loss_of(rc, "cpu").backward()
+        refs[tag] = sdr
+    _grad_compare(m.alignment_head, refs["bf"], refs["32"], "full model")
