@@ -112,10 +112,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="aggregator", choices=["aggregator", "chunk", "sequence"],
+    ap.add_argument("--workload", default="aggregator", choices=["aggregator", "chunk", "sequence", "train"],
                     help="aggregator: BASELINE configs[1] headline (default); chunk: full FeatureAlignedVGGT "
                          "per-chunk forward (encoder + alignment head + camera/depth heads); sequence: configs[2..4] "
-                         "chunk pipeline over --seq-frames frames (RCCL baton ring at N>1)")
+                         "chunk pipeline over --seq-frames frames (RCCL baton ring at N>1); train: one alignment-head "
+                         "training step (two chunks with memory recurrence, forward + backward + AdamW) on resident "
+                         "synthetic aggregator tokens (SURVEY §8f row 4)")
     ap.add_argument("--seq-frames", type=int, default=64)
     ap.add_argument("--height", type=int, default=H_IMG)
     ap.add_argument("--overlap", type=int, default=4)
@@ -138,6 +140,8 @@ def main():
     from aligned_vggt.backbone.aggregator import Aggregator
     from aligned_vggt.utils.synthetic import synthetic_images, synthetic_init_
 
+    if args.workload == "train":
+        return bench_train(args, world, rank, dev)
     if args.workload != "aggregator":
         return bench_full(args, world, rank, dev)
 
@@ -288,6 +292,70 @@ def bench_full(args, world, rank, dev):
                                             "seq_frames": args.seq_frames if args.workload == "sequence" else None,
                                             "image": [H, W], "heads": "camera+depth+alignment(memory 8)"}}),
               flush=True)
+
+
+def bench_train(args, world, rank, dev):
+    """Alignment-head training step (train_featureAlignedVGGT_vkitti.yaml: only
+    alignment_head.* trains, aggregator / camera / depth frozen): chunk 1
+    (first chunk) and chunk 2 (overlap tokens + memory from chunk 1) through
+    the head, a loss on both chunks' Sim(3) / SE(3) outputs and chunk 2's
+    memory, backward through the HIP training kernels, AdamW step.  The frozen
+    encoders' outputs (layer-23 tokens, (1, S, P, 2048) fp32) are synthetic and
+    resident in HBM.  Data-parallel over ranks (gradient all-reduce over RCCL
+    at N > 1, as Lightning DDP does)."""
+    import torch.distributed as dist
+    from aligned_vggt.heads.alignment_head import AlignmentHead
+    from aligned_vggt.utils.synthetic import synthetic_init_
+    H, W = args.height, W_IMG
+    S, ov = args.frames, args.overlap
+    P = 5 + (H // 14) * (W // 14)
+    head = AlignmentHead(in_dim=2048, num_memory_tokens=8).to(dev).train()
+    synthetic_init_(head, seed=0)
+    opt = torch.optim.AdamW(head.parameters(), lr=5e-5, weight_decay=0.05)
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    toks = [torch.randn(1, S, P, 2048, device=dev, generator=g) for _ in range(2)]
+    wcs = torch.randn(1, 1, 8, device=dev, generator=g)
+    wfs = torch.randn(1, S - 1, 7, device=dev, generator=g)
+
+    def step():
+        cs1, fs1, m1, o1 = head(toks[0], (H, W), ov)
+        cs2, fs2, m2, _ = head(toks[1], (H, W), ov, overlap_tokens=o1, memory_tokens=m1)
+        loss = ((cs1 + cs2) * wcs).sum() + ((fs1 + fs2) * wfs).sum() + m2.square().sum()
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        if world > 1:
+            for p in head.parameters():
+                if p.grad is not None:
+                    dist.all_reduce(p.grad)
+        torch.nn.utils.clip_grad_norm_(head.parameters(), 1.0)
+        opt.step()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+        dist.destroy_process_group()
+    if rank == 0:
+        value = 2 * world * args.steps / dt
+        print(json.dumps({
+            "metric": "chunks/sec (%d-frame %dx%d) alignment-head training (fwd+bwd+AdamW)" % (S, H, W),
+            "value": round(value, 4), "unit": "chunks/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (resident encoder tokens)",
+            "config": {"workload": "train", "frames": S, "overlap": ov, "image": [H, W],
+                       "chunks_per_step": 2, "parallelism": "dp%d" % world}}), flush=True)
 
 
 if __name__ == "__main__":

@@ -398,6 +398,14 @@ int vggt_resid_scale_add(float* x, int64_t ldx, const void* branch, int bdtype, 
 int vggt_transpose_b16(const void* src, int64_t lds, int rows, int cols, void* dst, int64_t ldd, int rows_pad,
                        void* stream);
 
+/* dW[n, k] (+)= bf16(sum_m dY[m, n] X[m, k]) for bf16 row-major dY [M, N], X [M, K] (the bf16-tier
+ * Linear weight gradients, rounded like autocast's bf16 weight gradient): split-K over the token
+ * dimension into fp32 partials in ws (>= vggt_wgrad_bf16_workspace_bytes), summed in split order.
+ * N % 128 == 0, K % 128 == 0. */
+size_t vggt_wgrad_bf16_workspace_bytes(int M, int N, int K);
+int vggt_wgrad_bf16(const void* dy, int64_t ldy, const void* x, int64_t ldx, int M, int N, int K, float* dw,
+                    int64_t ldw, int accumulate, void* ws, size_t ws_bytes, void* stream);
+
 /* dW[n, k] (+)= sum_m dY[m, n] X[m, k]  fp32 (skinny-M decoder / gated-update Linear weight gradients). */
 int vggt_wgrad_f32(const float* dy, int64_t ldy, const float* x, int64_t ldx, int M, int N, int K, float* dw,
                    int64_t ldw, int accumulate, void* stream);

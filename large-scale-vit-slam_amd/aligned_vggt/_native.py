@@ -76,10 +76,12 @@ _SIGS = {
     "vggt_resid_scale_add": [_vp, _i64, _vp, _i, _i64, _vp, _i, _i, _vp],
     "vggt_transpose_b16": [_vp, _i64, _i, _i, _vp, _i64, _i, _vp],
     "vggt_wgrad_f32": [_vp, _i64, _vp, _i64, _i, _i, _i, _vp, _i64, _i, _vp],
+    "vggt_wgrad_bf16": [_vp, _i64, _vp, _i64, _i, _i, _i, _vp, _i64, _i, _vp, ctypes.c_size_t, _vp],
     "vggt_batch_dot_f32": [_vp, _vp, _i64, _i, _i64, _vp, _vp, ctypes.c_size_t, _vp],
 }
 _WS_FNS = {"vggt_colred_workspace_bytes": [_i, _i], "vggt_layernorm_bwd_workspace_bytes": [_i, _i],
-           "vggt_headnorm_rope_bwd_workspace_bytes": [_i, _i], "vggt_batch_dot_workspace_bytes": [_i, _i64]}
+           "vggt_headnorm_rope_bwd_workspace_bytes": [_i, _i], "vggt_batch_dot_workspace_bytes": [_i, _i64],
+           "vggt_wgrad_bf16_workspace_bytes": [_i, _i, _i]}
 
 _lib = None
 
@@ -579,6 +581,19 @@ def transpose_b16(src, dst, rows_pad: int) -> None:
     assert src.element_size() == 2 and dst.element_size() == 2 and dst.shape[0] >= cols and dst.shape[1] >= rows_pad
     rc = lib().vggt_transpose_b16(_p(src), _ld(src), rows, cols, _p(dst), _ld(dst), rows_pad, _stream())
     _check(rc, "vggt_transpose_b16")
+
+
+def wgrad_bf16(dy, x, dw, accumulate: bool = False) -> None:
+    """dw[N, K] (+)= bf16-rounded dy[M, N]^T x[M, K] (bf16 row views, split-K MFMA)."""
+    _dev(dy, "wgrad_bf16")
+    M, N_ = dy.shape
+    K = x.shape[1]
+    assert x.shape[0] == M and dw.shape == (N_, K) and dw.dtype == torch.float32
+    L = lib()
+    ws = _train_ws(dy.device, int(L.vggt_wgrad_bf16_workspace_bytes(M, N_, K)))
+    rc = L.vggt_wgrad_bf16(_p(dy), _ld(dy), _p(x), _ld(x), M, N_, K, _p(dw), _ld(dw), int(accumulate), _p(ws),
+                           ws.numel() * 4, _stream())
+    _check(rc, "vggt_wgrad_bf16")
 
 
 def wgrad_f32(dy, x, dw, accumulate: bool = True) -> None:

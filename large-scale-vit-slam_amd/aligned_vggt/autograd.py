@@ -79,9 +79,11 @@ def _wt_f32(w: torch.Tensor, owner: nn.Module, name: str) -> torch.Tensor:
 
 
 class _LinBwd:
-    """bf16-tier Linear backward through the forward GEMM kernel:
-    dX = dY . W  (W^T packed once per weight version),
-    dW = dY^T . X (both operands transposed into zero-padded [*, Mp] bf16)."""
+    """bf16-tier Linear backward:
+    dX = dY . W  through the forward GEMM kernel (W^T packed once per weight version),
+    dW = dY^T . X by the split-K weight-gradient kernel (vggt_wgrad_bf16: row-major
+    operands, the token dimension as the MFMA reduction, no transposes); shapes
+    it does not cover go through transposed operands + the forward GEMM."""
 
     def __init__(self, ws: Workspace, M: int):
         self.ws = ws
@@ -95,6 +97,9 @@ class _LinBwd:
     def dw(self, dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> None:
         """out [N, K] fp32 = dy[M, N]^T x[M, K] (bf16-rounded like autocast's bf16 weight gradient)."""
         Nn, K = dy.shape[1], x.shape[1]
+        if Nn % 128 == 0 and K % 128 == 0:
+            N.wgrad_bf16(dy, x, out, False)
+            return
         a = self.ws.buf("tr_a", Nn, self.Mp, torch.bfloat16)
         b = self.ws.buf("tr_b", K, self.Mp, torch.bfloat16)
         N.transpose_b16(dy, a, self.Mp)

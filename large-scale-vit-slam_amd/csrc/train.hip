@@ -12,6 +12,7 @@
 #include <math.h>
 
 #include "common.h"
+#include "mfma_frag.h"
 
 namespace {
 
@@ -52,13 +53,27 @@ __device__ __forceinline__ float gelu_d(float x) {
 
 // ------------------------------------------------------------ finalize
 // out[i] (+)= sum_{c < nchunk} part[c * stride + i]   (fixed order)
+// Block = 16 columns x 16 chunk slices: slice s sums chunks s, s+16, ...
+// (independent loads in flight), then the 16 slice sums are added in slice
+// order through LDS -- the same order on every run.
 __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__ part, int nchunk, int n, int stride,
                                                        float* __restrict__ out, int accumulate) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
+  __shared__ float red[16][17];
+  const int col = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int i = blockIdx.x * 16 + col;
   float s = 0.f;
-  for (int c = 0; c < nchunk; ++c) s += part[(int64_t)c * stride + i];
-  out[i] = accumulate ? out[i] + s : s;
+  if (i < n) {
+#pragma unroll 4
+    for (int c = sl; c < nchunk; c += 16) s += part[(int64_t)c * stride + i];
+  }
+  red[sl][col] = s;
+  __syncthreads();
+  if (sl == 0 && i < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][col];
+    out[i] = accumulate ? out[i] + t : t;
+  }
 }
 
 // ------------------------------------------------------------ column sums
@@ -551,6 +566,103 @@ __global__ __launch_bounds__(256) void batch_dot_kernel(const float* __restrict_
   if (threadIdx.x == 0) part[(int64_t)blockIdx.x * B + b] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+
+// ------------------------------------------------------------ bf16 weight gradient (split-K over tokens)
+// part[z][n][k] = sum_{m in split z} dY[m][n] X[m][k]: both operands read
+// row-major from HBM (no transposes); the token dimension m is the MFMA
+// reduction, so both fragments come from ds_read_b64_tr_b16 transposed reads
+// of the padded [32 m][128] LDS tiles (vggt_frag::trfrag, the same k
+// permutation on A and B).  128x128 output tile per workgroup, 4 waves x
+// (64 x 64), double-buffered LDS, register-staged loads of tile t+1 in
+// flight during tile t's MFMAs.
+__global__ __launch_bounds__(256) void wgrad_bf16_kernel(const bf16_t* __restrict__ dy, int64_t ldy,
+                                                         const bf16_t* __restrict__ x, int64_t ldx, int M, int N,
+                                                         int K, int mchunk, float* __restrict__ part) {
+  using namespace vggt_frag;
+  constexpr int ROWP = Geo<128>::ROWP;
+  constexpr int TB = 32 * ROWP;
+  __shared__ __attribute__((aligned(16))) char smem[2][2 * TB];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ntn = N / 128;
+  const int n0 = (blockIdx.x % ntn) * 128, k0 = (blockIdx.x / ntn) * 128;
+  const int mb = blockIdx.y * mchunk, me = min(M, mb + mchunk);
+  const int wn = (wave >> 1) * 64, wk = (wave & 1) * 64;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+  // staging: 512 16-B chunks per operand tile; thread t moves chunks t and t+256
+  uint4 ry[2], rx[2];
+  auto load = [&](int m0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = threadIdx.x + 256 * i, row = c >> 4, ch = c & 15;
+      const int m = m0 + row;
+      ry[i] = m < me ? *(const uint4*)(dy + (int64_t)m * ldy + n0 + ch * 8) : uint4{0u, 0u, 0u, 0u};
+      rx[i] = m < me ? *(const uint4*)(x + (int64_t)m * ldx + k0 + ch * 8) : uint4{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = threadIdx.x + 256 * i, row = c >> 4, ch = c & 15;
+      *(uint4*)(&smem[buf][row * ROWP + ch * 16]) = ry[i];
+      *(uint4*)(&smem[buf][TB + row * ROWP + ch * 16]) = rx[i];
+    }
+  };
+  const int nt = (me - mb + 31) / 32;  // >= 1: the host never launches an empty split
+  load(mb);
+  store(0);
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nt) load(mb + (t + 1) * 32);
+    const char* ty = smem[cur];
+    const char* tx = smem[cur] + TB;
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        af[i] = trfrag<128>(ty, (wn >> 5) + i, 0, ss, lane);
+        bfr[i] = trfrag<128>(tx, (wk >> 5) + i, 0, ss, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < nt) store(cur ^ 1);
+    __syncthreads();
+  }
+  const int hl = lane >> 5;
+  float* pz = part + (int64_t)blockIdx.y * N * K;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = n0 + wn + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        const int k = k0 + wk + 32 * j + (lane & 31);
+        pz[(int64_t)n * K + k] = acc[i][j][r];
+      }
+}
+
+// out[n][k] (+)= round_bf16(sum_z part[z][n][k])  (fixed split order)
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int nz, int64_t nk,
+                                                           float* __restrict__ out, int64_t ldo, int K,
+                                                           int accumulate, int round) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nk) return;
+  float s = 0.f;
+  for (int z = 0; z < nz; ++z) s += part[(int64_t)z * nk + i];
+  if (round) s = round_bf(s);
+  float* o = out + (i / K) * ldo + (i % K);
+  *o = accumulate ? *o + s : s;
+}
+
 int nchunks_for(int M, int maxc) {
   int c = (M + 63) / 64;
   return c < 1 ? 1 : (c > maxc ? maxc : c);
@@ -574,7 +686,7 @@ extern "C" int vggt_colsum(const void* x, int dtype, int64_t ldx, int M, int N, 
   const int rpc = (M + nc - 1) / nc;
   dim3 grid((N / 4 + 255) / 256, nc);
   colred_kernel<0><<<grid, 256, 0, s>>>(x, dtype, ldx, nullptr, 0, 0, nullptr, nullptr, 0, 0, M, N, rpc, (float*)ws);
-  finalize_kernel<<<(N + 255) / 256, 256, 0, s>>>((const float*)ws, nc, N, N, out, accumulate);
+  finalize_kernel<<<(N + 15) / 16, 256, 0, s>>>((const float*)ws, nc, N, N, out, accumulate);
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
 }
@@ -592,8 +704,8 @@ extern "C" int vggt_layerscale_bwd(const float* dout, int64_t ldd, const void* b
   dim3 grid((N / 4 + 255) / 256, nc);
   colred_kernel<1><<<grid, 256, 0, s>>>(dout, VGGT_DTYPE_F32, ldd, branch, bdtype, ldb, gamma, dbranch, odtype, ldo,
                                         M, N, rpc, (float*)ws);
-  if (dgamma) finalize_kernel<<<(N + 255) / 256, 256, 0, s>>>((const float*)ws, nc, N, N, dgamma, 1);
-  if (dbias) finalize_kernel<<<(N + 255) / 256, 256, 0, s>>>((const float*)ws + (size_t)nc * N, nc, N, N, dbias, 1);
+  if (dgamma) finalize_kernel<<<(N + 15) / 16, 256, 0, s>>>((const float*)ws, nc, N, N, dgamma, 1);
+  if (dbias) finalize_kernel<<<(N + 15) / 16, 256, 0, s>>>((const float*)ws + (size_t)nc * N, nc, N, N, dbias, 1);
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
 }
@@ -621,7 +733,7 @@ extern "C" int vggt_gelu_bwd(const void* dh, int dhdtype, int64_t lddh, const vo
   dim3 grid((N / 4 + 255) / 256, nc);
   colred_kernel<2><<<grid, 256, 0, s>>>(dh, dhdtype, lddh, pre, predtype, ldp, nullptr, dpre, odtype, ldo, M, N, rpc,
                                         (float*)ws);
-  if (dbias) finalize_kernel<<<(N + 255) / 256, 256, 0, s>>>((const float*)ws, nc, N, N, dbias, 1);
+  if (dbias) finalize_kernel<<<(N + 15) / 16, 256, 0, s>>>((const float*)ws, nc, N, N, dbias, 1);
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
 }
@@ -673,8 +785,8 @@ extern "C" int vggt_layernorm_bwd(const void* x, int xdtype, int64_t ldx, const 
     case 4: launch_ln_bwd<4>(x, xdtype, ldx, w, eps, dy, dydtype, ldy, dx, dxdtype, lddx, accumulate, M, rm, nblk, rpb, part, s); break;
     default: return VGGT_ERR_SHAPE;
   }
-  if (dw) finalize_kernel<<<(C + 255) / 256, 256, 0, s>>>(part, nblk, C, C, dw, 1);
-  if (db) finalize_kernel<<<(C + 255) / 256, 256, 0, s>>>(part + (size_t)nblk * C, nblk, C, C, db, 1);
+  if (dw) finalize_kernel<<<(C + 15) / 16, 256, 0, s>>>(part, nblk, C, C, dw, 1);
+  if (db) finalize_kernel<<<(C + 15) / 16, 256, 0, s>>>(part + (size_t)nblk * C, nblk, C, C, db, 1);
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
 }
@@ -721,7 +833,7 @@ extern "C" int vggt_headnorm_rope_bwd(const void* pre, int64_t ldp, void* grad, 
     float* outs[4] = {dw0, db0, dw1, db1};
     // part layout [blk][a][D] -> finalize each (a) slice with stride 4*D per block
     for (int a = 0; a < 4; ++a)
-      if (outs[a]) finalize_kernel<<<(D + 255) / 256, 256, 0, s>>>(part + a * D, nblk, D, 4 * D, outs[a], 1);
+      if (outs[a]) finalize_kernel<<<(D + 15) / 16, 256, 0, s>>>(part + a * D, nblk, D, 4 * D, outs[a], 1);
   }
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
@@ -764,7 +876,36 @@ extern "C" int vggt_batch_dot_f32(const float* a, const float* c, int64_t bs, in
   const int64_t per = (n + nc - 1) / nc;
   hipStream_t s = (hipStream_t)stream;
   batch_dot_kernel<<<dim3((unsigned)nc, B), 256, 0, s>>>(a, c, bs, B, n, per, (float*)ws);
-  finalize_kernel<<<(B + 255) / 256, 256, 0, s>>>((const float*)ws, (int)nc, B, B, out, 0);
+  finalize_kernel<<<(B + 15) / 16, 256, 0, s>>>((const float*)ws, (int)nc, B, B, out, 0);
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+extern "C" size_t vggt_wgrad_bf16_workspace_bytes(int M, int N, int K) {
+  const int tiles = (N / 128) * (K / 128);
+  int splits = tiles >= 1024 ? 1 : (1024 + tiles - 1) / (tiles > 0 ? tiles : 1);
+  const int maxs = (M + 255) / 256;
+  if (splits > maxs) splits = maxs;
+  if (splits > 16) splits = 16;
+  if (splits < 1) splits = 1;
+  return (size_t)splits * N * K * sizeof(float);
+}
+
+extern "C" int vggt_wgrad_bf16(const void* dy, int64_t ldy, const void* x, int64_t ldx, int M, int N, int K, float* dw,
+                               int64_t ldw, int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || N % 128 || K % 128) return VGGT_ERR_SHAPE;
+  if ((ldy | ldx) % 8 || ((uintptr_t)dy | (uintptr_t)x) % 16) return VGGT_ERR_ALIGN;
+  const size_t need = vggt_wgrad_bf16_workspace_bytes(M, N, K);
+  if (!ws || ws_bytes < need) return VGGT_ERR_SHAPE;
+  const int splits = (int)(need / ((size_t)N * K * sizeof(float)));
+  int mchunk = (M + splits - 1) / splits;
+  mchunk = (mchunk + 31) / 32 * 32;
+  const int nz = (M + mchunk - 1) / mchunk;
+  hipStream_t s = (hipStream_t)stream;
+  wgrad_bf16_kernel<<<dim3((N / 128) * (K / 128), nz), 256, 0, s>>>((const bf16_t*)dy, ldy, (const bf16_t*)x, ldx, M,
+                                                                    N, K, mchunk, (float*)ws);
+  const int64_t nk = (int64_t)N * K;
+  wgrad_reduce_kernel<<<(unsigned)((nk + 255) / 256), 256, 0, s>>>((const float*)ws, nz, nk, dw, ldw, K, accumulate, 1);
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
 }

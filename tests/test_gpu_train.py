@@ -239,16 +239,32 @@ def test_transpose_wgrad_batchdot(N):
     assert _rel(out, (a * c).sum((1, 2, 3))) < 1e-5
 
 
-def test_bf16_weight_grad_gemm(N):
-    """dW = dY^T X through transposes + the forward GEMM (zero-padded token dim)."""
+@pytest.mark.parametrize("M,Nn,K", [(1000, 1024, 2048), (22000, 1024, 1024), (77, 4096, 1024), (5000, 3072, 1024)])
+def test_bf16_weight_grad(N, M, Nn, K):
+    """dW = dY^T X: split-K wgrad kernel on row-major operands (ragged token
+    count, strided dY), and the transposes + forward-GEMM form."""
     from aligned_vggt.autograd import _LinBwd
     from aligned_vggt.runtime import Workspace
     torch.manual_seed(7)
-    M, Nn, K = 1000, 1024, 2048
-    dy, x = _bf(torch.randn(M, Nn, device="cuda")), _bf(torch.randn(M, K, device="cuda"))
-    out = torch.empty(Nn, K, device="cuda")
-    _LinBwd(Workspace.get(torch.device("cuda", torch.cuda.current_device())), M).dw(dy, x, out)
-    assert _rel(out, dy.float().t() @ x.float()) < 4e-3
+    dyb = _bf(torch.randn(M, Nn + 128, device="cuda"))
+    dy, x = dyb[:, 64:64 + Nn], _bf(torch.randn(M, K, device="cuda"))
+    ref = dy.float().t() @ x.float()
+    out = torch.full((Nn, K), 3.0, device="cuda")
+    N.wgrad_bf16(dy, x, out, False)
+    assert _rel(out, ref) < 4e-3
+    N.wgrad_bf16(dy, x, out, True)
+    assert _rel(out, 2 * ref) < 4e-3
+    lb = _LinBwd(Workspace.get(torch.device("cuda", torch.cuda.current_device())), M)
+    out2 = torch.empty(Nn, K, device="cuda")
+    lb.dw(dy, x, out2)
+    assert _rel(out2, ref) < 4e-3
+    a = torch.empty(Nn, lb.Mp, device="cuda", dtype=torch.bfloat16)
+    b = torch.empty(K, lb.Mp, device="cuda", dtype=torch.bfloat16)
+    N.transpose_b16(dy, a, lb.Mp)
+    N.transpose_b16(x, b, lb.Mp)
+    out3 = torch.empty(Nn, K, device="cuda")
+    N.gemm_bf16(a, b, torch.zeros(K, device="cuda"), out3, N.EPI_F32)
+    assert _rel(out3, ref) < 4e-3
 
 
 # ------------------------------------------------------------------ blocks / head vs oracle autograd
