@@ -210,7 +210,8 @@ template <int BNX>
 __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf16_t* __restrict__ whi,
                                                             const bf16_t* __restrict__ wlo) {
   constexpr int NTN = BNX / 32;                       // 16-col fragments per wave (2 waves along N)
-  constexpr int WLD = BNX / 64;                       // 16-B W loads per thread per half
+  constexpr int WLD = BNX >= 64 ? BNX / 64 : 1;       // 16-B W loads per thread per half
+  const bool wact = BNX >= 64 || threadIdx.x < BNX * 4;  // BNX 32: threads 0-127 move the W tile
   constexpr int AT = BM * BK * 2, WT = BNX * BK * 2;  // bytes of one bf16 A / W tile
   constexpr int STG = 2 * AT + 2 * WT;               // Ahi, Alo, Whi, Wlo
   __shared__ __attribute__((aligned(16))) char smem[2 * STG];
@@ -241,10 +242,19 @@ __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf
   }
   // W: BNX rows x 32 K bf16 = BNX*64 B per half: row tid/4 + 64*i, chunk tid%4
   const int wr = tid >> 2, wch = tid & 3;
-  f32x4 ra[4];
-  uint4 rwh[WLD], rwl[WLD];
+  // two register staging sets: the loads of tile kt+2 are issued at the start
+  // of step kt and stored to LDS at the end of step kt+1, so every global /
+  // L2 gather has two MFMA steps to land
+  struct Stage {
+    f32x4 ra[4];
+    uint4 rwh[WLD], rwl[WLD];
+  };
+  Stage s0, s1;
 
-  auto load = [&](int kt) {
+  auto load = [&](Stage& st, int kt) {
+    f32x4 (&ra)[4] = st.ra;
+    uint4 (&rwh)[WLD] = st.rwh;
+    uint4 (&rwl)[WLD] = st.rwl;
     const int k0 = kt * BK;
     const int tap = k0 / a.ci;
     const int ci0 = k0 % a.ci + c4 * 4;
@@ -265,12 +275,16 @@ __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf
     }
 #pragma unroll
     for (int i = 0; i < WLD; ++i) {
+      if (!wact) break;
       const int64_t wo = (int64_t)(n0 + wr + 64 * i) * K + k0 + wch * 8;  // weights padded to a multiple of 128 rows
       rwh[i] = *(const uint4*)(whi + wo);
       rwl[i] = *(const uint4*)(wlo + wo);
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](const Stage& st, int buf) {
+    const f32x4 (&ra)[4] = st.ra;
+    const uint4 (&rwh)[WLD] = st.rwh;
+    const uint4 (&rwl)[WLD] = st.rwl;
     char* base = smem + buf * STG;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -289,6 +303,7 @@ __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf
     }
 #pragma unroll
     for (int i = 0; i < WLD; ++i) {
+      if (!wact) break;
       const int rr = wr + 64 * i;
       const int woff = rr * 64 + (swz64(rr, wch) << 4);
       *(uint4*)(base + 2 * AT + woff) = rwh[i];
@@ -305,12 +320,7 @@ __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf
 #pragma unroll
     for (int j = 0; j < NTN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  load(0);
-  store(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load(kt + 1);
+  auto compute = [&](int cur) {
     const char* base = smem + cur * STG;
     bf16x8 ah[4], al[4], bh[NTN], bl[NTN];
 #pragma unroll
@@ -333,9 +343,24 @@ __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mt], bl[nt], acc[mt][nt], 0, 0, 0);
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mt], bh[nt], acc[mt][nt], 0, 0, 0);
       }
-    if (kt + 1 < nk) store(cur ^ 1);
+  };
+
+  load(s0, 0);
+  store(s0, 0);
+  if (nk > 1) load(s1, 1);
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += 2) {
+    if (kt + 2 < nk) load(s0, kt + 2);
+    compute(0);
+    if (kt + 1 < nk) store(s1, 1);
+    __syncthreads();
+    if (kt + 1 >= nk) break;
+    if (kt + 3 < nk) load(s1, kt + 3);
+    compute(1);
+    if (kt + 2 < nk) store(s0, 0);
     __syncthreads();
   }
+
   conv_epilogue<NTN>(a, acc, M, m0, n0, wm, wn, r16, q);
 }
 
@@ -471,8 +496,10 @@ extern "C" int vggt_conv2d_bf16x3(const float* x, int64_t ldx, int nimg, int hi,
   if (a.ncols >= 128) {
     const int64_t nw2 = (nwg / ((a.ncols + BN - 1) / BN)) * ((a.ncols + 127) / 128);
     conv_bf16x3_kernel<128><<<(int)nw2, NT, 0, (hipStream_t)stream>>>(a, (const bf16_t*)w_hi, (const bf16_t*)w_lo);
-  } else {
+  } else if (a.ncols > 32) {
     conv_bf16x3_kernel<64><<<(int)nwg, NT, 0, (hipStream_t)stream>>>(a, (const bf16_t*)w_hi, (const bf16_t*)w_lo);
+  } else {  // output_conv2 (128 -> 32): 32-wide N tiles, no padded MFMA columns
+    conv_bf16x3_kernel<32><<<(int)nwg, NT, 0, (hipStream_t)stream>>>(a, (const bf16_t*)w_hi, (const bf16_t*)w_lo);
   }
   HIP_LAUNCH_CHECK();
   return VGGT_OK;

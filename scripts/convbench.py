@@ -1,0 +1,21 @@
+import sys, os, torch
+sys.path.insert(0, os.path.join(os.getcwd(), "large-scale-vit-slam_amd"))
+from aligned_vggt import _native as N
+dev = torch.device("cuda:0")
+def timeit(fn, reps=10):
+    fn(); torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps): fn()
+    b.record(); torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps * 1e3
+for (n, hw, ci, co) in [(16, 148, 256, 256), (16, 296, 256, 128), (16, 74, 256, 256), (16, 518, 128, 32)]:
+    x = torch.randn(n * hw * hw, ci, device=dev)
+    w = torch.randn(co, 9 * ci, device=dev) * 0.02
+    wp = torch.zeros((co + 127) // 128 * 128, 9 * ci, device=dev); wp[:co] = w
+    whi, wlo = N.split_bf16x2(wp)
+    b = torch.zeros(co, device=dev)
+    y = torch.empty(n * hw * hw, co, device=dev)
+    us = timeit(lambda: N.conv2d_bf16x3(x, n, hw, hw, ci, whi, wlo, b, co, 3, 3, 1, 1, y))
+    fl = 2 * n * hw * hw * co * 9 * ci
+    print(f"conv3x3 n={n} hw={hw} ci={ci} co={co}: {us:.1f} us  alg {fl/us/1e6:.0f} TF/s  mfma {3*fl/us/1e6:.0f} TF/s", flush=True)

@@ -52,7 +52,8 @@ def main():
         x = (torch.randn(M, 4096, device=dev) * 0.5).bfloat16()
         for mode, (name, Nn, K, epi) in [(md, sh) for md in map(int, args.gemm_modes.split(",")) for sh in (
                 ("qkv", 3 * C, C, N.EPI_BF16), ("proj", C, C, N.EPI_RESID_F32), ("fc1", 4 * C, C, N.EPI_GELU_BF16),
-                ("fc1_plain", 4 * C, C, N.EPI_BF16), ("fc2", C, 4 * C, N.EPI_RESID_F32))]:
+                ("fc1_plain", 4 * C, C, N.EPI_BF16), ("fc2", C, 4 * C, N.EPI_RESID_F32),
+                ("fc2_plain", C, 4 * C, N.EPI_BF16), ("proj_plain", C, C, N.EPI_BF16))]:
             N.tune(N.TUNE_GEMM_TILE, mode)
             w = (torch.randn(Nn, K, device=dev) * K ** -0.5).bfloat16()
             bias = torch.randn(Nn, device=dev) * 0.1
