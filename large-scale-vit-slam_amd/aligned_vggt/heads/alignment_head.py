@@ -119,8 +119,11 @@ class AlignmentHead(nn.Module):
         return pos.to(torch.int32).to(device), cos, sin
 
     def trainable(self) -> bool:
-        """Gradients requested for this head (training step, run_model.py:232)."""
-        return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+        """A training step for this head: train mode, autograd enabled and
+        trainable parameters (Lightning's training_step, run_model.py:232).
+        In eval mode the fused inference path runs and builds no graph, as
+        Lightning's validation / test steps run under no_grad anyway."""
+        return self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
 
     def forward(self, tokens: torch.Tensor, image_size: Tuple[int, int], next_num_overlap: int,
                 overlap_tokens: torch.Tensor = None, memory_tokens: torch.Tensor = None):
