@@ -196,6 +196,75 @@ __global__ __launch_bounds__(64) void attn_small_kernel(const T* __restrict__ q,
 }
 
 // ------------------------------------------------------------------------
+// Small-window attention, workgroup form: one 256-thread workgroup per
+// (group, head) with Q, K, V of the group staged once in LDS (fp32); the
+// nq x nk scores, the row softmaxes and the nq x D outputs are spread over
+// all 256 threads (a thread per score, per row, per output element), so no
+// query waits for another.  Same fp32 arithmetic and summation order as the
+// one-wave form above (serial over d for a score, over keys for an output).
+// Used when the group fits 64 KiB of LDS (temporal attention: 16 x <= 16
+// keys x 128; decoder / camera-head blocks).
+template <typename T>
+__global__ __launch_bounds__(256) void attn_small_wg_kernel(const T* __restrict__ q, int64_t ldq, int64_t qbs,
+                                                            const T* __restrict__ k, int64_t ldk, int64_t kbs,
+                                                            const T* __restrict__ v, int64_t ldv, T* __restrict__ o,
+                                                            int64_t ldo, int64_t obs, int heads, int nq, int nk, int D,
+                                                            float scale) {
+  extern __shared__ float sm[];
+  const int DP = D + 1;
+  float* Qs = sm;              // [nq][D+1]
+  float* Ks = Qs + nq * DP;    // [nk][D+1]
+  float* Vs = Ks + nk * DP;    // [nk][D]
+  float* Ps = Vs + nk * D;     // [nq][nk]
+  const int tid = threadIdx.x;
+  const int g = blockIdx.x / heads, h = blockIdx.x % heads;
+  const T* qp = q + (int64_t)g * qbs * ldq + h * D;
+  const T* kp = k + (int64_t)g * kbs * ldk + h * D;
+  const T* vp = v + (int64_t)g * kbs * ldv + h * D;
+  for (int i = tid; i < nq * D; i += 256) {
+    const int r = i / D, d = i % D;
+    Qs[r * DP + d] = ld1(qp + (int64_t)r * ldq + d);
+  }
+  for (int i = tid; i < nk * D; i += 256) {
+    const int r = i / D, d = i % D;
+    Ks[r * DP + d] = ld1(kp + (int64_t)r * ldk + d);
+    Vs[r * D + d] = ld1(vp + (int64_t)r * ldv + d);
+  }
+  __syncthreads();
+  for (int p = tid; p < nq * nk; p += 256) {
+    const int i = p / nk, j = p % nk;
+    const float* qr = Qs + i * DP;
+    const float* kr = Ks + j * DP;
+    float a = 0.f;
+    for (int d = 0; d < D; ++d) a = fmaf(qr[d], kr[d], a);
+    Ps[p] = a * scale;
+  }
+  __syncthreads();
+  for (int i = tid; i < nq; i += 256) {
+    float* pr = Ps + i * nk;
+    float m = -INFINITY;
+    for (int j = 0; j < nk; ++j) m = fmaxf(m, pr[j]);
+    float l = 0.f;
+    for (int j = 0; j < nk; ++j) {
+      const float e = expf(pr[j] - m);
+      pr[j] = e;
+      l += e;
+    }
+    const float inv = 1.f / l;
+    for (int j = 0; j < nk; ++j) pr[j] *= inv;
+  }
+  __syncthreads();
+  T* op = o + (int64_t)g * obs * ldo + h * D;
+  for (int p = tid; p < nq * D; p += 256) {
+    const int i = p / D, d = p % D;
+    const float* pr = Ps + i * nk;
+    float acc = 0.f;
+    for (int j = 0; j < nk; ++j) acc = fmaf(pr[j], Vs[j * D + d], acc);
+    st1(op + (int64_t)i * ldo + d, acc);
+  }
+}
+
+// ------------------------------------------------------------------------
 // fp32 per-head LayerNorm + RoPE (decoder / camera head run in fp32).
 template <int MODE>
 __global__ __launch_bounds__(64) void headnorm_rope_f32_kernel(float* __restrict__ buf, int64_t ld, int col_off,
@@ -336,6 +405,21 @@ extern "C" int vggt_attention_small(const void* q, int64_t ldq, int64_t q_bstrid
   }
   hipStream_t s = (hipStream_t)stream;
   const int grid = batch * heads;
+  const size_t lds_wg = ((size_t)(nq + nk) * (D + 1) + (size_t)nk * D + (size_t)nq * nk) * sizeof(float);
+  if (lds_wg <= 64 * 1024) {
+    if (dtype == VGGT_DTYPE_BF16)
+      attn_small_wg_kernel<bf16_t><<<grid, 256, lds_wg, s>>>((const bf16_t*)q, ldq, q_bstride, (const bf16_t*)k, ldk,
+                                                             k_bstride, (const bf16_t*)v, ldv, (bf16_t*)o, ldo,
+                                                             o_bstride, heads, nq, nk, D, scale);
+    else if (dtype == VGGT_DTYPE_F32)
+      attn_small_wg_kernel<float><<<grid, 256, lds_wg, s>>>((const float*)q, ldq, q_bstride, (const float*)k, ldk,
+                                                            k_bstride, (const float*)v, ldv, (float*)o, ldo, o_bstride,
+                                                            heads, nq, nk, D, scale);
+    else
+      return VGGT_ERR_UNSUPPORTED;
+    HIP_LAUNCH_CHECK();
+    return VGGT_OK;
+  }
   if (dtype == VGGT_DTYPE_BF16)
     attn_small_kernel<bf16_t><<<grid, 64, lds, s>>>((const bf16_t*)q, ldq, q_bstride, (const bf16_t*)k, ldk, k_bstride,
                                                     (const bf16_t*)v, ldv, (bf16_t*)o, ldo, o_bstride, heads, nq, nk,

@@ -446,11 +446,11 @@ __global__ __launch_bounds__(256) void headnorm_rope_bwd_kernel(const void* __re
 }
 
 // ------------------------------------------------------------ small attention backward
-// One workgroup (one wave) per (batch, head); everything in LDS as fp32:
+// One 256-thread workgroup per (batch, head); everything in LDS as fp32:
 // recompute S = q k^T * scale, P = softmax(S); dP = dO v^T;
 // dS = P * (dP - rowsum(P * dP)); dq = scale dS k; dk = scale dS^T q; dv = P^T dO.
 // (rowsum(P * dP) = rowsum(dO * O): the same delta without reading O.)
-__global__ __launch_bounds__(64) void attn_small_bwd_kernel(
+__global__ __launch_bounds__(256) void attn_small_bwd_kernel(
     const void* __restrict__ q, int64_t ldq, int64_t qbs, const void* __restrict__ k, int64_t ldk, int64_t kbs,
     const void* __restrict__ v, int64_t ldv, int64_t vbs, const void* __restrict__ dout, int64_t ldo, int64_t obs,
     void* __restrict__ dq, int64_t ldgq, int64_t gqbs, void* __restrict__ dk, void* __restrict__ dv, int64_t ldgk,
@@ -467,18 +467,18 @@ __global__ __launch_bounds__(64) void attn_small_bwd_kernel(
   auto ld1 = [&](const void* base, int64_t off) -> float {
     return dtype == VGGT_DTYPE_BF16 ? bf2f(((const bf16_t*)base)[off]) : ((const float*)base)[off];
   };
-  for (int i = lane; i < nq * D; i += 64) {
+  for (int i = lane; i < nq * D; i += 256) {
     const int r = i / D, c = i % D;
     sq[i] = ld1(q, ((int64_t)b * qbs + r) * ldq + h * D + c);
     sdo[i] = ld1(dout, ((int64_t)b * obs + r) * ldo + h * D + c);
   }
-  for (int i = lane; i < nk * D; i += 64) {
+  for (int i = lane; i < nk * D; i += 256) {
     const int r = i / D, c = i % D;
     sk[i] = ld1(k, ((int64_t)b * kbs + r) * ldk + h * D + c);
     sv[i] = ld1(v, ((int64_t)b * kbs + r) * ldv + h * D + c);
   }
   __syncthreads();
-  for (int i = lane; i < nq * nk; i += 64) {
+  for (int i = lane; i < nq * nk; i += 256) {
     const int r = i / nk, c = i % nk;
     float s = 0.f, t = 0.f;
     for (int d = 0; d < D; ++d) {
@@ -489,7 +489,7 @@ __global__ __launch_bounds__(64) void attn_small_bwd_kernel(
     sdp[i] = t;
   }
   __syncthreads();
-  for (int r = lane; r < nq; r += 64) {
+  for (int r = lane; r < nq; r += 256) {
     float m = -INFINITY;
     for (int c = 0; c < nk; ++c) m = fmaxf(m, sp[r * nk + c]);
     float l = 0.f;
@@ -517,13 +517,13 @@ __global__ __launch_bounds__(64) void attn_small_bwd_kernel(
     if (dtype == VGGT_DTYPE_BF16) ((bf16_t*)base)[off] = f2bf(val);
     else ((float*)base)[off] = val;
   };
-  for (int i = lane; i < nq * D; i += 64) {
+  for (int i = lane; i < nq * D; i += 256) {
     const int r = i / D, c = i % D;
     float s = 0.f;
     for (int j = 0; j < nk; ++j) s += sp[r * nk + j] * sk[j * D + c];
     st1(dq, ((int64_t)b * gqbs + r) * ldgq + h * D + c, s * scale);
   }
-  for (int i = lane; i < nk * D; i += 64) {
+  for (int i = lane; i < nk * D; i += 256) {
     const int r = i / D, c = i % D;
     float s = 0.f, t = 0.f;
     for (int j = 0; j < nq; ++j) {
@@ -848,7 +848,7 @@ extern "C" int vggt_attention_small_bwd(const void* q, int64_t ldq, int64_t q_bs
   if (dtype != VGGT_DTYPE_F32 && dtype != VGGT_DTYPE_BF16) return VGGT_ERR_UNSUPPORTED;
   const size_t lds = ((size_t)2 * nq * D + (size_t)2 * nk * D + (size_t)2 * nq * nk) * sizeof(float);
   if (lds > 64 * 1024) return VGGT_ERR_SHAPE;
-  attn_small_bwd_kernel<<<batch * heads, 64, lds, (hipStream_t)stream>>>(
+  attn_small_bwd_kernel<<<batch * heads, 256, lds, (hipStream_t)stream>>>(
       q, ldq, q_bstride, k, ldk, k_bstride, v, ldv, k_bstride, dout, ldo, o_bstride, dq, lddq, dq_bstride, dk, dv,
       lddkv, dkv_bstride, dtype, heads, nq, nk, D, scale);
   HIP_LAUNCH_CHECK();
