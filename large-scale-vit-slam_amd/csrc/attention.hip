@@ -154,14 +154,15 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
     voff[i] = (uint32_t)(row * a.ldv + v_swz<D>(row, cp) * 8) * 2u;
   }
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem)) + wave * IPW * 1024;
-  const uint64_t kstep = (uint64_t)BKV * a.ldk * 2, vstep = (uint64_t)BKV * a.ldv * 2;
-  const uint64_t kbytes = (uint64_t)a.nk * a.ldk * 2, vbytes = (uint64_t)a.nk * a.ldv * 2;
+  // 32-bit scalar descriptor arithmetic (host: nk * ld * 2 < 2^31): a 64-bit
+  // "remaining bytes" compare has no SALU form and would run on the VALU
+  const int kstep = BKV * (int)a.ldk * 2, vstep = BKV * (int)a.ldv * 2;
+  const int kbytes = a.nk * (int)a.ldk * 2, vbytes = a.nk * (int)a.ldv * 2;
 
   auto stage = [&](int buf, int t) {
-    const uint64_t ko = kstep * t, vo = vstep * t;
-    const uint64_t kr_n = kbytes > ko ? kbytes - ko : 0, vr_n = vbytes > vo ? vbytes - vo : 0;
-    const int32x4 kr = make_rsrc((const char*)kp + ko, (uint32_t)(kr_n > 0xffffffffull ? 0xffffffffull : kr_n));
-    const int32x4 vr = make_rsrc((const char*)vp + vo, (uint32_t)(vr_n > 0xffffffffull ? 0xffffffffull : vr_n));
+    const int ko = kstep * t, vo = vstep * t;
+    const int32x4 kr = make_rsrc((const char*)kp + ko, (uint32_t)max(kbytes - ko, 0));
+    const int32x4 vr = make_rsrc((const char*)vp + vo, (uint32_t)max(vbytes - vo, 0));
     const uint32_t d = lds0 + buf * 2 * TILEB;
 #pragma unroll
     for (int i = 0; i < IPW; ++i) {
@@ -527,8 +528,8 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
   if (D != 64 && D != 128) return VGGT_ERR_UNSUPPORTED;
   if ((ldq | ldk | ldv | ldo) % 8 || ((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) % 16)
     return VGGT_ERR_ALIGN;
-  // per-lane 32-bit DMA offsets: one 64-row tile must span < 2 GiB
-  if ((uint64_t)BKV * (uint64_t)(ldk > ldv ? ldk : ldv) * 2 >= (1ull << 31)) return VGGT_ERR_SHAPE;
+  // 32-bit DMA offsets and descriptor arithmetic: K / V of one (batch, head) must span < 2 GiB
+  if ((uint64_t)nk * (uint64_t)(ldk > ldv ? ldk : ldv) * 2 >= (1ull << 31)) return VGGT_ERR_SHAPE;
   AttnArgs a{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, ldq, ldk, ldv, ldo,
              q_bstride, k_bstride, v_bstride, o_bstride, batch, heads, nq, nk,
              scale * 1.4426950408889634f, nullptr};
@@ -594,7 +595,7 @@ extern "C" int vggt_attention_fwd_lse(const void* q, int64_t ldq, int64_t q_bstr
   if (D != 64 && D != 128) return VGGT_ERR_UNSUPPORTED;
   if ((ldq | ldk | ldv | ldo) % 8 || ((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) % 16)
     return VGGT_ERR_ALIGN;
-  if ((uint64_t)BKV * (uint64_t)(ldk > ldv ? ldk : ldv) * 2 >= (1ull << 31)) return VGGT_ERR_SHAPE;
+  if ((uint64_t)nk * (uint64_t)(ldk > ldv ? ldk : ldv) * 2 >= (1ull << 31)) return VGGT_ERR_SHAPE;
   AttnArgs a{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, ldq, ldk, ldv, ldo,
              q_bstride, k_bstride, v_bstride, o_bstride, batch, heads, nq, nk,
              scale * 1.4426950408889634f, lse};

@@ -4,6 +4,7 @@
 // camera-head attention over <= 128 tokens), fp32 QK-norm + RoPE, casts and
 // row-remapped LayerNorm.  See include/vggt_mi355x.h for the contracts.
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.h"
 
@@ -406,7 +407,8 @@ extern "C" int vggt_attention_small(const void* q, int64_t ldq, int64_t q_bstrid
   hipStream_t s = (hipStream_t)stream;
   const int grid = batch * heads;
   const size_t lds_wg = ((size_t)(nq + nk) * (D + 1) + (size_t)nk * D + (size_t)nq * nk) * sizeof(float);
-  if (lds_wg <= 64 * 1024) {
+  static const int use_wg = getenv("VGGT_ATTN_SMALL_WG") ? atoi(getenv("VGGT_ATTN_SMALL_WG")) : 1;
+  if (use_wg && lds_wg <= 64 * 1024) {
     if (dtype == VGGT_DTYPE_BF16)
       attn_small_wg_kernel<bf16_t><<<grid, 256, lds_wg, s>>>((const bf16_t*)q, ldq, q_bstride, (const bf16_t*)k, ldk,
                                                              k_bstride, (const bf16_t*)v, ldv, (bf16_t*)o, ldo,
