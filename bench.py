@@ -323,10 +323,15 @@ def bench_train(args, world, rank, dev):
         loss = ((cs1 + cs2) * wcs).sum() + ((fs1 + fs2) * wfs).sum() + m2.square().sum()
         opt.zero_grad(set_to_none=True)
         loss.backward()
-        if world > 1:
-            for p in head.parameters():
-                if p.grad is not None:
-                    dist.all_reduce(p.grad)
+        if world > 1:  # one bucketed all-reduce of every gradient over RCCL (DDP semantics: mean)
+            grads = [p.grad for p in head.parameters() if p.grad is not None]
+            flat = torch.cat([g.reshape(-1) for g in grads])
+            dist.all_reduce(flat)
+            flat /= world
+            off = 0
+            for g_ in grads:
+                g_.copy_(flat[off:off + g_.numel()].view_as(g_))
+                off += g_.numel()
         torch.nn.utils.clip_grad_norm_(head.parameters(), 1.0)
         opt.step()
 
