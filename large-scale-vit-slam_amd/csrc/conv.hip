@@ -206,17 +206,31 @@ __global__ __launch_bounds__(NT, 2) void conv_f32_kernel(ConvArgs a) {
 // ===========================================================================
 __device__ __forceinline__ int swz64(int row, int chunk) { return chunk ^ ((4 - ((row >> 2) & 3)) & 3); }
 
+typedef int int32x4c __attribute__((ext_vector_type(4)));
+
+// 16 B per lane from (rsrc, voff + soff) into LDS at the wave-uniform address
+// `lds` (+ lane * 16): buffer_load ... lds (LDS-DMA).  In asm so the
+// compiler does not drain vmcnt around it; completion is waited for
+// explicitly before the barrier that publishes the stage.
+__device__ __forceinline__ void cdma16(int32x4c rsrc, uint32_t voff, uint32_t soff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds)
+               : "memory");
+}
+
 template <int BNX>
 __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf16_t* __restrict__ whi,
                                                             const bf16_t* __restrict__ wlo) {
   constexpr int NTN = BNX / 32;                       // 16-col fragments per wave (2 waves along N)
-  constexpr int WLD = BNX >= 64 ? BNX / 64 : 1;       // 16-B W loads per thread per half
-  const bool wact = BNX >= 64 || threadIdx.x < BNX * 4;  // BNX 32: threads 0-127 move the W tile
   constexpr int AT = BM * BK * 2, WT = BNX * BK * 2;  // bytes of one bf16 A / W tile
   constexpr int STG = 2 * AT + 2 * WT;               // Ahi, Alo, Whi, Wlo
+  constexpr int WPW = WT / 1024 / 4 > 0 ? WT / 1024 / 4 : 1;  // W DMA pieces per wave per half (BNX 32: waves 0-1)
   __shared__ __attribute__((aligned(16))) char smem[2 * STG];
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int M = a.nimg * a.ho * a.wo;
   const int tiles_n = (a.ncols + BNX - 1) / BNX;
   const int tiles_m = (M + BM - 1) / BM;
@@ -225,6 +239,14 @@ __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf
   const int n0 = (t % tiles_n) * BNX;
   const int K = a.kh * a.kw * a.ci;
   const int nk = K / BK;
+  // K-step order: channel slice outer, tap inner.  Step s covers tap s % ntap
+  // and channels (s / ntap)*32 .. +32, i.e. weight columns tap*ci + slice*32
+  // (the (ky, kx, ci) weight layout is unchanged).  The ntap consecutive steps
+  // of one slice gather overlapping input windows (3x3 shifts of the same
+  // pixels and channels), so the gather hits L2 instead of re-streaming the
+  // activation from HBM once per tap.
+  const int ntap = a.kh * a.kw;
+  auto kcol = [&](int s) { return (s % ntap) * a.ci + (s / ntap) * BK; };
 
   // A: rows r = tid/8 + 32*i, fp32 channel quad c4 = tid%8 (4 K values)
   const int c4 = tid & 7;
@@ -240,74 +262,82 @@ __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf
     py[i] = (rem / a.wo) * a.stride - a.pad;
     px[i] = (rem % a.wo) * a.stride - a.pad;
   }
-  // W: BNX rows x 32 K bf16 = BNX*64 B per half: row tid/4 + 64*i, chunk tid%4
-  const int wr = tid >> 2, wch = tid & 3;
-  // two register staging sets: the loads of tile kt+2 are issued at the start
-  // of step kt and stored to LDS at the end of step kt+1, so every global /
-  // L2 gather has two MFMA steps to land
+  // W (pre-split bf16, rows padded to a multiple of 128) by LDS-DMA: piece p
+  // (1 KiB) of a half = rows 16p..16p+15 (64-B rows); lane -> row 16p + lane/4,
+  // LDS chunk lane%4, which must hold global chunk (lane%4) ^ h(row) -- the
+  // swz64 swizzle applied on the source address (the DMA image is lane-linear).
+  const bool wdma = wave * WPW * 1024 < WT;
+  uint32_t woff[WPW];
+#pragma unroll
+  for (int i = 0; i < WPW; ++i) {
+    const int row = (wave * WPW + i) * 16 + (lane >> 2);
+    const int g = swz64(row, lane & 3);
+    woff[i] = (uint32_t)(row * K + g * 8) * 2u;
+  }
+  int32x4c rwh, rwl;
+  {
+    const uint64_t bh = (uint64_t)(whi + (int64_t)n0 * K), bl = (uint64_t)(wlo + (int64_t)n0 * K);
+    rwh[0] = __builtin_amdgcn_readfirstlane((uint32_t)bh);
+    rwh[1] = __builtin_amdgcn_readfirstlane((uint32_t)(bh >> 32)) & 0xffff;
+    rwl[0] = __builtin_amdgcn_readfirstlane((uint32_t)bl);
+    rwl[1] = __builtin_amdgcn_readfirstlane((uint32_t)(bl >> 32)) & 0xffff;
+    rwh[2] = rwl[2] = -1;
+    rwh[3] = rwl[3] = 0x00020000;
+  }
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem));
+  auto wstage = [&](int buf, int kt) {
+    if (!wdma) return;
+    const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(kcol(kt) * 2));
+    const uint32_t b = lds0 + buf * STG + 2 * AT + wave * WPW * 1024;
+#pragma unroll
+    for (int i = 0; i < WPW; ++i) {
+      cdma16(rwh, woff[i], soff, b + i * 1024);
+      cdma16(rwl, woff[i], soff, b + WT + i * 1024);
+    }
+  };
+  // A gather staged through registers, one K-step ahead: issued at the start
+  // of step kt, split and stored at its end (no use of the loaded values in
+  // between -- the input ReLU is applied at the store -- so the loads stay in
+  // flight during the MFMAs)
   struct Stage {
     f32x4 ra[4];
-    uint4 rwh[WLD], rwl[WLD];
   };
-  Stage s0, s1;
+  Stage s0;
 
   auto load = [&](Stage& st, int kt) {
     f32x4 (&ra)[4] = st.ra;
-    uint4 (&rwh)[WLD] = st.rwh;
-    uint4 (&rwl)[WLD] = st.rwl;
-    const int k0 = kt * BK;
-    const int tap = k0 / a.ci;
-    const int ci0 = k0 % a.ci + c4 * 4;
+    const int tap = kt % ntap;
+    const int ci0 = (kt / ntap) * BK + c4 * 4;
     const int ky = tap / a.kw, kx = tap % a.kw;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int iy = py[i] + ky, ix = px[i] + kx;
-      if (pv[i] && iy >= 0 && iy < a.hi && ix >= 0 && ix < a.wi) {
-        f32x4 v = *(const f32x4*)(a.x + (((int64_t)pn[i] * a.hi + iy) * a.wi + ix) * a.ldx + ci0);
-        if (a.relu_in) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
-        }
-        ra[i] = v;
-      } else {
-        ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < WLD; ++i) {
-      if (!wact) break;
-      const int64_t wo = (int64_t)(n0 + wr + 64 * i) * K + k0 + wch * 8;  // weights padded to a multiple of 128 rows
-      rwh[i] = *(const uint4*)(whi + wo);
-      rwl[i] = *(const uint4*)(wlo + wo);
+      // no use of the loaded value here (the input ReLU is applied at the
+      // store): the gather stays in flight for two MFMA steps
+      ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (pv[i] && iy >= 0 && iy < a.hi && ix >= 0 && ix < a.wi)
+        ra[i] = *(const f32x4*)(a.x + (((int64_t)pn[i] * a.hi + iy) * a.wi + ix) * a.ldx + ci0);
     }
   };
   auto store = [&](const Stage& st, int buf) {
-    const f32x4 (&ra)[4] = st.ra;
-    const uint4 (&rwh)[WLD] = st.rwh;
-    const uint4 (&rwl)[WLD] = st.rwl;
     char* base = smem + buf * STG;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = (tid >> 3) + 32 * i;
       uint2 h, l;
-      float hv[4];
+      float xv[4], hv[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) hv[j] = round_bf(ra[i][j]);
+      for (int j = 0; j < 4; ++j) {
+        xv[j] = a.relu_in ? fmaxf(st.ra[i][j], 0.f) : st.ra[i][j];
+        hv[j] = round_bf(xv[j]);
+      }
       h.x = pack_bf2(hv[0], hv[1]);
       h.y = pack_bf2(hv[2], hv[3]);
-      l.x = pack_bf2(ra[i][0] - hv[0], ra[i][1] - hv[1]);
-      l.y = pack_bf2(ra[i][2] - hv[2], ra[i][3] - hv[3]);
+      l.x = pack_bf2(xv[0] - hv[0], xv[1] - hv[1]);
+      l.y = pack_bf2(xv[2] - hv[2], xv[3] - hv[3]);
       const int off = r * 64 + (swz64(r, c4 >> 1) << 4) + (c4 & 1) * 8;
       *(uint2*)(base + off) = h;
       *(uint2*)(base + AT + off) = l;
-    }
-#pragma unroll
-    for (int i = 0; i < WLD; ++i) {
-      if (!wact) break;
-      const int rr = wr + 64 * i;
-      const int woff = rr * 64 + (swz64(rr, wch) << 4);
-      *(uint4*)(base + 2 * AT + woff) = rwh[i];
-      *(uint4*)(base + 2 * AT + WT + woff) = rwl[i];
     }
   };
 
@@ -345,19 +375,24 @@ __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf
       }
   };
 
+  // Per step kt (LDS buffer kt & 1): W DMA of tile kt+1 into the other
+  // buffer, the A gather of tile kt+1 into registers, the MFMAs of tile kt,
+  // the split + store of A tile kt+1, then every wave's DMA retired
+  // (vmcnt(0)) before the barrier that publishes the next buffer.
+  wstage(0, 0);
   load(s0, 0);
   store(s0, 0);
-  if (nk > 1) load(s1, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int kt = 0; kt < nk; kt += 2) {
-    if (kt + 2 < nk) load(s0, kt + 2);
-    compute(0);
-    if (kt + 1 < nk) store(s1, 1);
-    __syncthreads();
-    if (kt + 1 >= nk) break;
-    if (kt + 3 < nk) load(s1, kt + 3);
-    compute(1);
-    if (kt + 2 < nk) store(s0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      wstage(cur ^ 1, kt + 1);
+      load(s0, kt + 1);
+    }
+    compute(cur);
+    if (kt + 1 < nk) store(s0, cur ^ 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
