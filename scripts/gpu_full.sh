@@ -16,6 +16,7 @@ if [ -z "${SKIP_TESTS:-}" ]; then
 fi
 step bench 900 python bench.py --steps 5 --warmup 2 || exit $?
 step bench_chunk 900 python bench.py --workload chunk --steps 5 --warmup 2 --no-cpu-baseline || exit $?
+step bench_train 900 python bench.py --workload train --steps 5 --warmup 2 || exit $?
 step prof 900 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit $?
 step prof_chunk 900 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_chunk" -o run -- python3 bench.py --workload chunk --steps 2 --warmup 1 --no-cpu-baseline || exit $?
 step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline || exit $?
