@@ -71,6 +71,14 @@ int vggt_gemm_bf16(const void* A, int64_t lda, const void* W, int64_t ldw, const
                    int epi, void* out, int64_t ldo, const float* gamma, float* out2, int64_t ldo2, void* stream);
 
 /*
+ * vggt_gemm_bf16 with VGGT_EPI_GELU_BF16 that also stores the bf16 pre-activation A.W^T + bias to `pre`
+ * (row stride ldp): the training recompute of Mlp.fc1 -> GELU keeps both for the GELU backward
+ * (alignment_head.py:351-393 under checkpoint), in one pass instead of a GEMM + a separate GELU kernel.
+ */
+int vggt_gemm_bf16_gelu_pre(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int M, int N,
+                            int K, void* out, int64_t ldo, void* pre, int64_t ldp, void* stream);
+
+/*
  * Fused attention input projection: qkv[M, 3*H*D] = bf16(A . W^T + bias), then,
  * in the same epilogue, the q and k column blocks get the per-head LayerNorm
  * (q_norm / k_norm: weights [D], eps; NULL weights = no norm) and RoPE
@@ -118,6 +126,20 @@ int vggt_headnorm_rope(void* buf, int64_t ld, int col_off, int M, int H, int D, 
 int vggt_qknorm_rope(void* qkv, int64_t ld, int M, int H, int D, const float* qw, const float* qb, const float* kw,
                      const float* kb, float eps, int rope_mode, const int32_t* pos, int period, const float* cos_tab,
                      const float* sin_tab, int tab_len, void* stream);
+
+/*
+ * Out-of-place forms (training recompute, alignment_head.py:351-393 under checkpoint: the backward needs the
+ * pre-norm projections, so they are not overwritten): heads are read from src (row stride lds) and the
+ * normalised + rotated values written to dst (row stride ldd).  vggt_qknorm_rope_out covers the q|k columns
+ * [0, 2*H*D) of a fused projection, vggt_headnorm_rope_out H heads from column 0.
+ */
+int vggt_qknorm_rope_out(const void* src, int64_t lds, void* dst, int64_t ldd, int M, int H, int D, const float* qw,
+                         const float* qb, const float* kw, const float* kb, float eps, int rope_mode,
+                         const int32_t* pos, int period, const float* cos_tab, const float* sin_tab, int tab_len,
+                         void* stream);
+int vggt_headnorm_rope_out(const void* src, int64_t lds, void* dst, int64_t ldd, int M, int H, int D, const float* w,
+                           const float* b, float eps, int rope_mode, const int32_t* pos, int period,
+                           const float* cos_tab, const float* sin_tab, int tab_len, void* stream);
 
 /*
  * Flash attention forward, bf16 in/out, fp32 online softmax, D in {64,128}.
@@ -392,6 +414,10 @@ int vggt_gelu_bwd(const void* dh, int dhdtype, int64_t lddh, const void* pre, in
 /* x_f32[m, n] += gamma[n] * branch[m, n]  (LayerScale residual add with a saved branch). */
 int vggt_resid_scale_add(float* x, int64_t ldx, const void* branch, int bdtype, int64_t ldb, const float* gamma, int M,
                          int N, void* stream);
+
+/* out_f32[m, n] = x_f32[m, n] + gamma[n] * branch[m, n]  (out may equal x). */
+int vggt_resid_scale_add_from(float* out, int64_t ldo, const float* x, int64_t ldx, const void* branch, int bdtype,
+                              int64_t ldb, const float* gamma, int M, int N, void* stream);
 
 /* dst[c, r] = src[r, c] for 2-byte elements; columns r in [rows, rows_pad) of dst are zero
  * (weight-gradient GEMM operands: dW = dY^T X as vggt_gemm_bf16(dY^T, X^T)). */

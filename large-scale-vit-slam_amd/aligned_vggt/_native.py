@@ -74,6 +74,10 @@ _SIGS = {
     "vggt_gelu_fwd": [_vp, _i, _i64, _vp, _i, _i64, _i, _i, _vp],
     "vggt_gelu_bwd": [_vp, _i, _i64, _vp, _i, _i64, _vp, _i, _i64, _i, _i, _vp, _vp, ctypes.c_size_t, _vp],
     "vggt_resid_scale_add": [_vp, _i64, _vp, _i, _i64, _vp, _i, _i, _vp],
+    "vggt_gemm_bf16_gelu_pre": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _vp, _i64, _vp, _i64, _vp],
+    "vggt_resid_scale_add_from": [_vp, _i64, _vp, _i64, _vp, _i, _i64, _vp, _i, _i, _vp],
+    "vggt_qknorm_rope_out": [_vp, _i64, _vp, _i64, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _i, _vp, _i, _vp, _vp, _i, _vp],
+    "vggt_headnorm_rope_out": [_vp, _i64, _vp, _i64, _i, _i, _i, _vp, _vp, _f, _i, _vp, _i, _vp, _vp, _i, _vp],
     "vggt_transpose_b16": [_vp, _i64, _i, _i, _vp, _i64, _i, _vp],
     "vggt_wgrad_f32": [_vp, _i64, _vp, _i64, _i, _i, _i, _vp, _i64, _i, _vp],
     "vggt_wgrad_bf16": [_vp, _i64, _vp, _i64, _i, _i, _i, _vp, _i64, _i, _vp, ctypes.c_size_t, _vp],
@@ -170,6 +174,21 @@ def gemm_bf16(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out: torch.T
     return out
 
 
+def gemm_bf16_gelu_pre(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out: torch.Tensor,
+                       pre: torch.Tensor) -> torch.Tensor:
+    """out = GELU(a . w^T + bias) and pre = a . w^T + bias, both bf16 (one pass)."""
+    _dev(a, "gemm_bf16_gelu_pre")
+    M, K = a.shape
+    N_ = w.shape[0]
+    assert a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.shape[1] == K
+    assert out.shape[0] == M and out.shape[1] == N_ and pre.shape[0] == M and pre.shape[1] == N_
+    assert out.dtype == torch.bfloat16 and pre.dtype == torch.bfloat16
+    rc = lib().vggt_gemm_bf16_gelu_pre(_p(a), _ld(a), _p(w), _ld(w), _p(bias), M, N_, K, _p(out), _ld(out), _p(pre),
+                                       _ld(pre), _stream())
+    _check(rc, "vggt_gemm_bf16_gelu_pre")
+    return out
+
+
 def gemm_qkv(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out: torch.Tensor, H: int, D: int, qw=None, qb=None,
              kw=None, kb=None, eps: float = 0.0, mode: int = ROPE_NONE, pos=None, period: int = 1, cos=None,
              sin=None) -> torch.Tensor:
@@ -215,6 +234,30 @@ def qknorm_rope(qkv: torch.Tensor, H: int, D: int, qw, qb, kw, kb, eps: float, m
     rc = lib().vggt_qknorm_rope(_p(qkv), _ld(qkv), qkv.shape[0], H, D, _p(qw), _p(qb), _p(kw), _p(kb), float(eps), mode,
                                 _p(pos), period, _p(cos), _p(sin), tab, _stream())
     _check(rc, "vggt_qknorm_rope")
+
+
+def qknorm_rope_out(src: torch.Tensor, dst: torch.Tensor, H: int, D: int, qw, qb, kw, kb, eps: float,
+                    mode: int = ROPE_NONE, pos=None, period: int = 1, cos=None, sin=None) -> None:
+    """dst[:, :2HD] = q/k-norm + RoPE of src[:, :2HD] (src untouched)."""
+    _dev(src, "qknorm_rope_out")
+    assert src.dtype == torch.bfloat16 and dst.dtype == torch.bfloat16 and dst.shape[0] == src.shape[0]
+    assert src.shape[1] >= 2 * H * D and dst.shape[1] >= 2 * H * D
+    tab = cos.shape[0] if cos is not None else 0
+    rc = lib().vggt_qknorm_rope_out(_p(src), _ld(src), _p(dst), _ld(dst), src.shape[0], H, D, _p(qw), _p(qb), _p(kw),
+                                    _p(kb), float(eps), mode, _p(pos), period, _p(cos), _p(sin), tab, _stream())
+    _check(rc, "vggt_qknorm_rope_out")
+
+
+def headnorm_rope_out(src: torch.Tensor, dst: torch.Tensor, H: int, D: int, w, b, eps: float, mode: int = ROPE_NONE,
+                      pos=None, period: int = 1, cos=None, sin=None) -> None:
+    """dst[:, :HD] = per-head norm + RoPE of src[:, :HD] (src untouched)."""
+    _dev(src, "headnorm_rope_out")
+    assert src.dtype == torch.bfloat16 and dst.dtype == torch.bfloat16 and dst.shape[0] == src.shape[0]
+    assert src.shape[1] >= H * D and dst.shape[1] >= H * D
+    tab = cos.shape[0] if cos is not None else 0
+    rc = lib().vggt_headnorm_rope_out(_p(src), _ld(src), _p(dst), _ld(dst), src.shape[0], H, D, _p(w), _p(b),
+                                      float(eps), mode, _p(pos), period, _p(cos), _p(sin), tab, _stream())
+    _check(rc, "vggt_headnorm_rope_out")
 
 
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, o: torch.Tensor, batch: int, heads: int, nq: int,
@@ -572,6 +615,16 @@ def resid_scale_add(x, branch, gamma) -> None:
     M, N_ = x.shape
     rc = lib().vggt_resid_scale_add(_p(x), _ld(x), _p(branch), _dt(branch), _ld(branch), _p(gamma), M, N_, _stream())
     _check(rc, "vggt_resid_scale_add")
+
+
+def resid_scale_add_from(out, x, branch, gamma) -> None:
+    """out = x + gamma * branch (fp32 out / x; out may be x)."""
+    _dev(x, "resid_scale_add_from")
+    M, N_ = x.shape
+    assert out.shape == x.shape and out.dtype == torch.float32 and x.dtype == torch.float32
+    rc = lib().vggt_resid_scale_add_from(_p(out), _ld(out), _p(x), _ld(x), _p(branch), _dt(branch), _ld(branch),
+                                         _p(gamma), M, N_, _stream())
+    _check(rc, "vggt_resid_scale_add_from")
 
 
 def transpose_b16(src, dst, rows_pad: int) -> None:

@@ -123,9 +123,8 @@ def _mlp_fwd(blk, x1: torch.Tensor, ws: Workspace, pfx: str):
     N.layernorm(x1, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps, xn2)
     w1, b1 = pack_linear(blk.mlp.fc1)
     hpre = ws.buf(pfx + "hpre", M, w1.shape[0], torch.bfloat16)
-    N.gemm_bf16(xn2, w1, b1, hpre, N.EPI_BF16)
     h = ws.buf(pfx + "h", M, w1.shape[0], torch.bfloat16)
-    N.gelu_fwd(hpre, h)
+    N.gemm_bf16_gelu_pre(xn2, w1, b1, h, hpre)  # GELU in the epilogue, pre-activation kept for the backward
     w2, b2 = pack_linear(blk.mlp.fc2)
     br2 = ws.buf(pfx + "br2", M, C, torch.bfloat16)
     N.gemm_bf16(h, w2, b2, br2, N.EPI_BF16)
@@ -164,25 +163,28 @@ class FrameBlockFn(torch.autograd.Function):
         w, b = pack_linear(blk.attn.qkv)
         qpre = ws.buf("fb_qkvpre", M, 3 * C, torch.bfloat16)
         N.gemm_bf16(xn1, w, b, qpre, N.EPI_BF16)
-        qkv = ws.buf("fb_qkv", M, 3 * C, torch.bfloat16)
-        qkv.copy_(qpre)
         qn, kn = blk.attn.q_norm, blk.attn.k_norm
         has_norm = isinstance(qn, nn.LayerNorm)
         mode = rope.mode if (rope is not None and blk.attn.rope is not None) else N.ROPE_NONE
         if has_norm or mode != N.ROPE_NONE:
-            N.qknorm_rope(qkv, H, D, qn.weight if has_norm else None, qn.bias if has_norm else None,
-                          kn.weight if has_norm else None, kn.bias if has_norm else None,
-                          qn.eps if has_norm else 0.0, mode, rope.pos if mode else None, rope.period if mode else 1,
-                          rope.cos if mode else None, rope.sin if mode else None)
+            # q|k normalised out of place (the backward needs the pre-norm
+            # values); v is read from the projection itself
+            qk = ws.buf("fb_qk", M, 2 * C, torch.bfloat16)
+            N.qknorm_rope_out(qpre, qk, H, D, qn.weight if has_norm else None, qn.bias if has_norm else None,
+                              kn.weight if has_norm else None, kn.bias if has_norm else None,
+                              qn.eps if has_norm else 0.0, mode, rope.pos if mode else None,
+                              rope.period if mode else 1, rope.cos if mode else None, rope.sin if mode else None)
+            qkv = (qk[:, :C], qk[:, C:], qpre[:, 2 * C:])
+        else:
+            qkv = (qpre[:, :C], qpre[:, C:2 * C], qpre[:, 2 * C:])
         ao = ws.buf("fb_ao", M, C, torch.bfloat16)
         lse = ws.buf("fb_lse", 1, nb * H * rows, torch.float32)
-        N.attention_fwd_lse(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], ao, lse, nb, H, rows, rows, D, rows, rows, rows)
+        N.attention_fwd_lse(qkv[0], qkv[1], qkv[2], ao, lse, nb, H, rows, rows, D, rows, rows, rows)
         wp, bp = pack_linear(blk.attn.proj)
         br1 = ws.buf("fb_br1", M, C, torch.bfloat16)
         N.gemm_bf16(ao, wp, bp, br1, N.EPI_BF16)
         x1 = ws.buf("fb_x1", M, C, torch.float32)
-        x1.copy_(x)
-        N.resid_scale_add(x1, br1, blk.ls1.gamma.detach())
+        N.resid_scale_add_from(x1, x, br1, blk.ls1.gamma.detach())
         xn2, hpre, h, br2 = _mlp_fwd(blk, x1, ws, "fb_")
         return dict(xn1=xn1, qpre=qpre, qkv=qkv, ao=ao, lse=lse, br1=br1, x1=x1, xn2=xn2, hpre=hpre, h=h, br2=br2,
                     has_norm=has_norm, mode=mode)
@@ -191,8 +193,8 @@ class FrameBlockFn(torch.autograd.Function):
     def forward(ctx, x, blk, groups, rope, *params):
         ws = Workspace.get(x.device)
         t = FrameBlockFn._recompute(blk, x, groups, rope, ws)
-        out = t["x1"].clone()
-        N.resid_scale_add(out, t["br2"], blk.ls2.gamma.detach())
+        out = torch.empty_like(t["x1"])
+        N.resid_scale_add_from(out, t["x1"], t["br2"], blk.ls2.gamma.detach())
         ctx.save_for_backward(x)
         ctx.blk, ctx.groups, ctx.rope = blk, groups, rope
         return out
@@ -231,7 +233,7 @@ class FrameBlockFn(torch.autograd.Function):
         lb.dx(dbr, blk.attn.proj, dao)
         qkv = t["qkv"]
         dqkv = ws.buf("fbb_dqkv", M, 3 * C, torch.bfloat16)
-        N.attention_bwd(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], t["ao"], dao, t["lse"], dqkv[:, :C],
+        N.attention_bwd(qkv[0], qkv[1], qkv[2], t["ao"], dao, t["lse"], dqkv[:, :C],
                         dqkv[:, C:2 * C], dqkv[:, 2 * C:], nb, H, rows, rows, D, rows, rows, rows)
         mode = t["mode"]
         if t["has_norm"] or mode != N.ROPE_NONE:
@@ -287,34 +289,37 @@ class TemporalBlockFn(torch.autograd.Function):
         wkv, bkv = blk.attn.packed_kv()
         kvpre = ws.buf("tb_kvpre", My, 2 * C, torch.bfloat16)
         N.gemm_bf16(yn, wkv, bkv, kvpre, N.EPI_BF16)
-        q = ws.buf("tb_q", Mx, C, torch.bfloat16)
-        q.copy_(qpre)
-        kv = ws.buf("tb_kv", My, 2 * C, torch.bfloat16)
-        kv.copy_(kvpre)
         mode = N.ROPE_1D if blk.attn.rope is not None else N.ROPE_NONE
-        for buf, which, rp in ((q, "q", rq), (kv, "k", rk)):
+        q, k = qpre, kvpre[:, :C]
+        for which, rp, src, nm in (("q", rq, qpre, "tb_q"), ("k", rk, kvpre, "tb_k")):
             w, b, eps = blk._qk_norm(which)
             if w is not None or mode != N.ROPE_NONE:
-                N.headnorm_rope(buf, 0, H, D, w, b, eps, mode, rp[0] if mode else None, rp[0].numel() if mode else 1,
-                                rp[1] if mode else None, rp[2] if mode else None)
+                # normalised out of place: the backward needs the pre-norm projections
+                dst = ws.buf(nm, src.shape[0], C, torch.bfloat16)
+                N.headnorm_rope_out(src, dst, H, D, w, b, eps, mode, rp[0] if mode else None,
+                                    rp[0].numel() if mode else 1, rp[1] if mode else None, rp[2] if mode else None)
+                if which == "q":
+                    q = dst
+                else:
+                    k = dst
+        v = kvpre[:, C:]
         ao = ws.buf("tb_ao", Mx, C, torch.bfloat16)
-        N.attention_small(q, kv[:, :C], kv[:, C:], ao, groups, H, nq, nk, D, nq, nk, nq)
+        N.attention_small(q, k, v, ao, groups, H, nq, nk, D, nq, nk, nq)
         wp, bp = pack_linear(blk.attn.proj)
         br1 = ws.buf("tb_br1", Mx, C, torch.bfloat16)
         N.gemm_bf16(ao, wp, bp, br1, N.EPI_BF16)
         x1 = ws.buf("tb_x1", Mx, C, torch.float32)
-        x1.copy_(x)
-        N.resid_scale_add(x1, br1, blk.ls1.gamma.detach())
+        N.resid_scale_add_from(x1, x, br1, blk.ls1.gamma.detach())
         xn2, hpre, h, br2 = _mlp_fwd(blk, x1, ws, "tb_")
-        return dict(ysrc=ysrc, xn1=xn1, yn=yn, qpre=qpre, kvpre=kvpre, q=q, kv=kv, ao=ao, br1=br1, x1=x1, xn2=xn2,
+        return dict(ysrc=ysrc, xn1=xn1, yn=yn, qpre=qpre, kvpre=kvpre, q=q, k=k, v=v, ao=ao, br1=br1, x1=x1, xn2=xn2,
                     hpre=hpre, h=h, br2=br2, mode=mode)
 
     @staticmethod
     def forward(ctx, x, y, blk, groups, nq, nk, rq, rk, *params):
         ws = Workspace.get(x.device)
         t = TemporalBlockFn._recompute(blk, x, y, groups, nq, nk, rq, rk, ws)
-        out = t["x1"].clone()
-        N.resid_scale_add(out, t["br2"], blk.ls2.gamma.detach())
+        out = torch.empty_like(t["x1"])
+        N.resid_scale_add_from(out, t["x1"], t["br2"], blk.ls2.gamma.detach())
         if y is None:
             ctx.save_for_backward(x)
         else:
@@ -360,10 +365,9 @@ class TemporalBlockFn(torch.autograd.Function):
         lb.dw(dbr, t["ao"], g["proj.w"])
         dao = ws.buf("tbb_dxn", Mx, C, torch.bfloat16)
         lb.dx(dbr, blk.attn.proj, dao)
-        q, kv = t["q"], t["kv"]
         dq = ws.buf("tbb_dq", Mx, C, torch.bfloat16)
         dkv = ws.buf("tbb_dkv", My, 2 * C, torch.bfloat16)
-        N.attention_small_bwd(q, kv[:, :C], kv[:, C:], dao, dq, dkv[:, :C], dkv[:, C:], groups, H, nq, nk, D, nq, nk,
+        N.attention_small_bwd(t["q"], t["k"], t["v"], dao, dq, dkv[:, :C], dkv[:, C:], groups, H, nq, nk, D, nq, nk,
                               nq, nq, nk)
         mode = t["mode"]
         if has_norm or mode != N.ROPE_NONE:

@@ -114,9 +114,19 @@ class AlignmentHead(nn.Module):
             self.__dict__["_mi355x_rope2d"] = c
         return c[1]
 
+    def _i32(self, pos: torch.Tensor, device) -> torch.Tensor:
+        """Device int32 copy of a small host position vector, cached per value
+        (a per-chunk host->device copy would synchronise the stream)."""
+        cache = self.__dict__.setdefault("_mi355x_pos", {})
+        key = (tuple(pos.tolist()), str(device))
+        c = cache.get(key)
+        if c is None:
+            c = cache[key] = pos.to(torch.int32).to(device)
+        return c
+
     def _rope1d(self, pos: torch.Tensor, dim: int, device):
         cos, sin = self.rope1d.tables(dim, int(pos.max()), device)
-        return pos.to(torch.int32).to(device), cos, sin
+        return self._i32(pos, device), cos, sin
 
     def trainable(self) -> bool:
         """A training step for this head: train mode, autograd enabled and
@@ -220,7 +230,7 @@ class AlignmentHead(nn.Module):
         hd = dec // self.num_heads
         maxp = int(max(cross.max(), seq.max() if S > 1 else 0))
         tabs = self.rope1d.tables(hd, maxp, dev)
-        i32 = lambda t: t.to(torch.int32).to(dev)
+        i32 = lambda t: self._i32(t, dev)
         tok = AG.linear_f32(self.project_dec, frame_alignment_tokens.float())
         tok = AG.layernorm_f32(self.dec_norm, tok)
         directional = None
@@ -338,7 +348,7 @@ class AlignmentHead(nn.Module):
         hd = dec // self.num_heads
         maxp = int(max(cross.max(), seq.max() if S > 1 else 0))
         tabs = self.rope1d.tables(hd, maxp, dev)
-        i32 = lambda t: t.to(torch.int32).to(dev)
+        i32 = lambda t: self._i32(t, dev)
 
         ft = frame_alignment_tokens.reshape(B * S, Ce).float().contiguous()
         tok = torch.empty(B * S, dec, device=dev)

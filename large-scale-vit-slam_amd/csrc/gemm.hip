@@ -167,6 +167,8 @@ __device__ __forceinline__ void write_tile(const char* Cs, int m0, int n0, int M
         v[2 * j + 1] = bf2f((bf16_t)(w4[j] >> 16));
       }
       if constexpr (EPI == VGGT_EPI_GELU_BF16) {
+        // the pre-activation (bf16 Linear output) for the GELU backward
+        if (ep.out2) *(uint4*)((bf16_t*)(void*)ep.out2 + (int64_t)m * ep.ldo2 + n) = cv;
         uint4 o;
         const f32x2 g0 = gelu_fast2(f32x2{v[0], v[1]}), g1 = gelu_fast2(f32x2{v[2], v[3]});
         const f32x2 g2 = gelu_fast2(f32x2{v[4], v[5]}), g3 = gelu_fast2(f32x2{v[6], v[7]});
@@ -242,9 +244,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(const bf16_t* __restri
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
+  auto compute = [&](int cur) {
     const char* As = smem + cur * STAGE_BYTES;
     const char* Ws = As + TILE;
 #pragma unroll
@@ -263,9 +263,31 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(const bf16_t* __restri
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi) acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], af[mi], acc[ni][mi], 0, 0, 0);
     }
+  };
+  for (int kt = 0; kt < nk - 1; ++kt) {
+    stage((kt & 1) ^ 1, (kt + 1) * BK);
+    compute(kt & 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+  // LayerScale + residual epilogue: this thread's fp32 residual rows (the
+  // write_tile mapping) are loaded now, all at once, so their HBM latency hides
+  // behind the last K-step and the C-tile staging instead of serialising the
+  // read-modify-write passes at the end
+  constexpr int RCPR = BN / 8, RRPP = NT / RCPR, RNP = BM / RRPP;
+  f32x4 rx[RNP][2];
+  if constexpr (EPI == VGGT_EPI_RESID_F32) {
+    const int n = n0 + (threadIdx.x % RCPR) * 8;
+#pragma unroll
+    for (int i = 0; i < RNP; ++i) {
+      const int m = min(m0 + (int)threadIdx.x / RCPR + RRPP * i, M - 1);
+      const float* xp = (const float*)ep.out + (int64_t)m * ep.ldo + n;
+      rx[i][0] = __builtin_nontemporal_load((const f32x4*)xp);
+      rx[i][1] = __builtin_nontemporal_load((const f32x4*)(xp + 4));
+    }
+  }
+  compute((nk - 1) & 1);
+  __syncthreads();
 
   // ---- epilogue 1: acc (C^T fragments) + bias -> bf16 C tile in LDS ----
   char* Cs = smem;
@@ -299,6 +321,37 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(const bf16_t* __restri
       write_tile<EPI, BM, BN, NT, CROW>(Cs, m0, n0, M, ep, ts, ts + tab);
       return;
     }
+  }
+  if constexpr (EPI == VGGT_EPI_RESID_F32) {
+    const int ch = threadIdx.x % RCPR;
+    const int n = n0 + ch * 8;
+    const f32x4 g0 = *(const f32x4*)(ep.gamma + n);
+    const f32x4 g1 = *(const f32x4*)(ep.gamma + n + 4);
+#pragma unroll
+    for (int i = 0; i < RNP; ++i) {
+      const int ml = threadIdx.x / RCPR + RRPP * i;
+      const int m = m0 + ml;
+      if (m >= M) continue;
+      const uint4 cv = *(const uint4*)(Cs + ml * CROW + ch * 16);
+      const uint32_t w4[4] = {cv.x, cv.y, cv.z, cv.w};
+      f32x4 x0 = rx[i][0], x1 = rx[i][1];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        x0[2 * j] += g0[2 * j] * bf2f((bf16_t)(w4[j] & 0xffff));
+        x0[2 * j + 1] += g0[2 * j + 1] * bf2f((bf16_t)(w4[j] >> 16));
+        x1[2 * j] += g1[2 * j] * bf2f((bf16_t)(w4[2 + j] & 0xffff));
+        x1[2 * j + 1] += g1[2 * j + 1] * bf2f((bf16_t)(w4[2 + j] >> 16));
+      }
+      float* xp = (float*)ep.out + (int64_t)m * ep.ldo + n;
+      *(f32x4*)xp = x0;
+      *(f32x4*)(xp + 4) = x1;
+      if (ep.out2) {
+        float* yp = ep.out2 + (int64_t)m * ep.ldo2 + n;
+        *(f32x4*)yp = x0;
+        *(f32x4*)(yp + 4) = x1;
+      }
+    }
+    return;
   }
   write_tile<EPI, BM, BN, NT, CROW>(Cs, m0, n0, M, ep);
 }
@@ -721,14 +774,16 @@ inline int pp_pick_bn(int M, int N, bool allow192) {
 
 }  // namespace
 
-extern "C" int vggt_gemm_bf16(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int M, int N,
-                              int K, int epi, void* out, int64_t ldo, const float* gamma, float* out2, int64_t ldo2,
-                              void* stream) {
+namespace {
+int gemm_impl(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int M, int N, int K, int epi,
+              void* out, int64_t ldo, const float* gamma, float* out2, int64_t ldo2, void* stream) {
   if (M <= 0 || N <= 0 || K <= 0 || N % 128 || K % 32) return VGGT_ERR_SHAPE;
   if ((lda % 8) || (ldw % 8) || ((uintptr_t)A & 15) || ((uintptr_t)W & 15) || ((uintptr_t)bias & 15))
     return VGGT_ERR_ALIGN;
   if (epi == VGGT_EPI_RESID_F32 && (!gamma || ((uintptr_t)gamma & 15) || (out2 && (ldo2 % 4))))
     return VGGT_ERR_ALIGN;
+  if (epi == VGGT_EPI_GELU_BF16 && out2 && ((ldo2 % 8) || ((uintptr_t)out2 & 15))) return VGGT_ERR_ALIGN;
+  if (epi != VGGT_EPI_RESID_F32 && epi != VGGT_EPI_GELU_BF16) out2 = nullptr;
   if ((epi == VGGT_EPI_BF16 || epi == VGGT_EPI_GELU_BF16) ? (ldo % 8) : (ldo % 4)) return VGGT_ERR_ALIGN;
   Epi ep{bias, out, ldo, gamma, out2, ldo2};
   hipStream_t s = (hipStream_t)stream;
@@ -804,6 +859,19 @@ extern "C" int vggt_gemm_bf16(const void* A, int64_t lda, const void* W, int64_t
   }
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
+}
+}  // namespace
+
+extern "C" int vggt_gemm_bf16(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int M, int N,
+                              int K, int epi, void* out, int64_t ldo, const float* gamma, float* out2, int64_t ldo2,
+                              void* stream) {
+  return gemm_impl(A, lda, W, ldw, bias, M, N, K, epi, out, ldo, gamma, epi == VGGT_EPI_RESID_F32 ? out2 : nullptr,
+                   ldo2, stream);
+}
+
+extern "C" int vggt_gemm_bf16_gelu_pre(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int M,
+                                       int N, int K, void* out, int64_t ldo, void* pre, int64_t ldp, void* stream) {
+  return gemm_impl(A, lda, W, ldw, bias, M, N, K, VGGT_EPI_GELU_BF16, out, ldo, nullptr, (float*)pre, ldp, stream);
 }
 
 extern "C" int vggt_gemm_qkv(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int M, int H,

@@ -97,8 +97,11 @@ int launch_ln(const void* x, int in_bf, int64_t ldx, const float* w, const float
 // a head; LPH = D/8 lanes per head, heads processed 64/LPH at a time.
 // Heads [0, hsplit) use (w, b), heads [hsplit, H) use (w2, b2): one launch
 // normalises q and k of a fused qkv row (different q_norm / k_norm weights).
+// Rows are read from src (row stride lds; == buf for the in-place form) and
+// written to buf, at the same column offset.
 template <int D, int MODE>
-__global__ __launch_bounds__(256) void headnorm_rope_kernel(bf16_t* __restrict__ buf, int64_t ld, int col_off, int M,
+__global__ __launch_bounds__(256) void headnorm_rope_kernel(const bf16_t* src, int64_t lds, bf16_t* buf, int64_t ld,
+                                                            int col_off, int M,
                                                             int H, const float* __restrict__ w,
                                                             const float* __restrict__ b, float eps,
                                                             const int32_t* __restrict__ pos, int period,
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(256) void headnorm_rope_kernel(bf16_t* __restrict__
     bf16_t* p = buf + (int64_t)row * ld + col_off + (act ? h : 0) * D + e0;
     float x[8];
     {
-      const uint4 u = *(const uint4*)p;
+      const uint4 u = *(const uint4*)(src + (int64_t)row * lds + col_off + (act ? h : 0) * D + e0);
       const uint32_t uu[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -200,21 +203,21 @@ __global__ __launch_bounds__(256) void headnorm_rope_kernel(bf16_t* __restrict__
 }
 
 template <int D>
-int launch_hnr(bf16_t* buf, int64_t ld, int col_off, int M, int H, const float* w, const float* b, float eps, int mode,
+int launch_hnr(const bf16_t* src, int64_t lds, bf16_t* buf, int64_t ld, int col_off, int M, int H, const float* w, const float* b, float eps, int mode,
                const int32_t* pos, int period, const float* cs, const float* sn, int tab_len, hipStream_t s,
                int hsplit, const float* w2, const float* b2) {
   const int grid = (M + 3) / 4;
   switch (mode) {
     case VGGT_ROPE_NONE:
-      headnorm_rope_kernel<D, VGGT_ROPE_NONE><<<grid, 256, 0, s>>>(buf, ld, col_off, M, H, w, b, eps, pos, period, cs,
+      headnorm_rope_kernel<D, VGGT_ROPE_NONE><<<grid, 256, 0, s>>>(src, lds, buf, ld, col_off, M, H, w, b, eps, pos, period, cs,
                                                                   sn, tab_len, hsplit, w2, b2);
       break;
     case VGGT_ROPE_2D:
-      headnorm_rope_kernel<D, VGGT_ROPE_2D><<<grid, 256, 0, s>>>(buf, ld, col_off, M, H, w, b, eps, pos, period, cs, sn,
+      headnorm_rope_kernel<D, VGGT_ROPE_2D><<<grid, 256, 0, s>>>(src, lds, buf, ld, col_off, M, H, w, b, eps, pos, period, cs, sn,
                                                                 tab_len, hsplit, w2, b2);
       break;
     case VGGT_ROPE_1D:
-      headnorm_rope_kernel<D, VGGT_ROPE_1D><<<grid, 256, 0, s>>>(buf, ld, col_off, M, H, w, b, eps, pos, period, cs, sn,
+      headnorm_rope_kernel<D, VGGT_ROPE_1D><<<grid, 256, 0, s>>>(src, lds, buf, ld, col_off, M, H, w, b, eps, pos, period, cs, sn,
                                                                 tab_len, hsplit, w2, b2);
       break;
     default: return VGGT_ERR_UNSUPPORTED;
@@ -267,9 +270,9 @@ extern "C" int vggt_headnorm_rope(void* buf, int64_t ld, int col_off, int M, int
   if (rope_mode != VGGT_ROPE_NONE && (!pos || !cos_tab || !sin_tab || period <= 0 || tab_len <= 0))
     return VGGT_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
-  if (D == 64) return launch_hnr<64>((bf16_t*)buf, ld, col_off, M, H, w, b, eps, rope_mode, pos, period, cos_tab, sin_tab,
+  if (D == 64) return launch_hnr<64>((const bf16_t*)buf, ld, (bf16_t*)buf, ld, col_off, M, H, w, b, eps, rope_mode, pos, period, cos_tab, sin_tab,
                                      tab_len, s, H, w, b);
-  return launch_hnr<128>((bf16_t*)buf, ld, col_off, M, H, w, b, eps, rope_mode, pos, period, cos_tab, sin_tab, tab_len, s,
+  return launch_hnr<128>((const bf16_t*)buf, ld, (bf16_t*)buf, ld, col_off, M, H, w, b, eps, rope_mode, pos, period, cos_tab, sin_tab, tab_len, s,
                          H, w, b);
 }
 
@@ -283,8 +286,47 @@ extern "C" int vggt_qknorm_rope(void* qkv, int64_t ld, int M, int H, int D, cons
   if (rope_mode != VGGT_ROPE_NONE && (!pos || !cos_tab || !sin_tab || period <= 0 || tab_len <= 0))
     return VGGT_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
-  if (D == 64) return launch_hnr<64>((bf16_t*)qkv, ld, 0, M, 2 * H, qw, qb, eps, rope_mode, pos, period, cos_tab,
+  if (D == 64) return launch_hnr<64>((const bf16_t*)qkv, ld, (bf16_t*)qkv, ld, 0, M, 2 * H, qw, qb, eps, rope_mode, pos, period, cos_tab,
                                      sin_tab, tab_len, s, H, kw, kb);
-  return launch_hnr<128>((bf16_t*)qkv, ld, 0, M, 2 * H, qw, qb, eps, rope_mode, pos, period, cos_tab, sin_tab, tab_len,
+  return launch_hnr<128>((const bf16_t*)qkv, ld, (bf16_t*)qkv, ld, 0, M, 2 * H, qw, qb, eps, rope_mode, pos, period, cos_tab, sin_tab, tab_len,
                          s, H, kw, kb);
+}
+
+// Out-of-place form of vggt_qknorm_rope: the q|k columns [0, 2*H*D) of src
+// (row stride lds) are normalised + rotated into dst (row stride ldd); src is
+// left untouched (the training recompute keeps the pre-norm values for the
+// backward, and the v columns are read from src directly).
+extern "C" int vggt_qknorm_rope_out(const void* src, int64_t lds, void* dst, int64_t ldd, int M, int H, int D,
+                                    const float* qw, const float* qb, const float* kw, const float* kb, float eps,
+                                    int rope_mode, const int32_t* pos, int period, const float* cos_tab,
+                                    const float* sin_tab, int tab_len, void* stream) {
+  if (M <= 0) return M == 0 ? VGGT_OK : VGGT_ERR_SHAPE;
+  if (H <= 0 || (D != 64 && D != 128)) return VGGT_ERR_SHAPE;
+  if ((lds % 8) || (ldd % 8) || ((uintptr_t)src % 16) || ((uintptr_t)dst % 16)) return VGGT_ERR_ALIGN;
+  if ((qw == nullptr) != (kw == nullptr)) return VGGT_ERR_SHAPE;
+  if (rope_mode != VGGT_ROPE_NONE && (!pos || !cos_tab || !sin_tab || period <= 0 || tab_len <= 0))
+    return VGGT_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  if (D == 64) return launch_hnr<64>((const bf16_t*)src, lds, (bf16_t*)dst, ldd, 0, M, 2 * H, qw, qb, eps, rope_mode,
+                                     pos, period, cos_tab, sin_tab, tab_len, s, H, kw, kb);
+  return launch_hnr<128>((const bf16_t*)src, lds, (bf16_t*)dst, ldd, 0, M, 2 * H, qw, qb, eps, rope_mode, pos, period,
+                         cos_tab, sin_tab, tab_len, s, H, kw, kb);
+}
+
+// Out-of-place form of vggt_headnorm_rope: H heads of D columns starting at
+// column 0 of src (row stride lds) normalised + rotated into dst (row stride ldd).
+extern "C" int vggt_headnorm_rope_out(const void* src, int64_t lds, void* dst, int64_t ldd, int M, int H, int D,
+                                      const float* w, const float* b, float eps, int rope_mode, const int32_t* pos,
+                                      int period, const float* cos_tab, const float* sin_tab, int tab_len,
+                                      void* stream) {
+  if (M <= 0) return M == 0 ? VGGT_OK : VGGT_ERR_SHAPE;
+  if (H <= 0 || (D != 64 && D != 128)) return VGGT_ERR_SHAPE;
+  if ((lds % 8) || (ldd % 8) || ((uintptr_t)src % 16) || ((uintptr_t)dst % 16)) return VGGT_ERR_ALIGN;
+  if (rope_mode != VGGT_ROPE_NONE && (!pos || !cos_tab || !sin_tab || period <= 0 || tab_len <= 0))
+    return VGGT_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  if (D == 64) return launch_hnr<64>((const bf16_t*)src, lds, (bf16_t*)dst, ldd, 0, M, H, w, b, eps, rope_mode, pos,
+                                     period, cos_tab, sin_tab, tab_len, s, H, w, b);
+  return launch_hnr<128>((const bf16_t*)src, lds, (bf16_t*)dst, ldd, 0, M, H, w, b, eps, rope_mode, pos, period,
+                         cos_tab, sin_tab, tab_len, s, H, w, b);
 }

@@ -147,10 +147,11 @@ __global__ __launch_bounds__(256) void colred_kernel(const void* __restrict__ a,
 
 // ------------------------------------------------------------ elementwise
 // MODE 0: y = bf16/f32(GELU(x))           (unfused fc1 activation, training recompute)
-// MODE 1: x_f32 += gamma * y              (LayerScale residual add with a saved branch)
+// MODE 1: x_f32 = src_f32 + gamma * y     (LayerScale residual add with a saved branch; src == x in place)
 template <int MODE>
-__global__ __launch_bounds__(256) void ew_kernel(const void* __restrict__ x, int xdt, int64_t ldx, void* __restrict__ y,
-                                                 int ydt, int64_t ldy, const float* __restrict__ gamma, int M, int N) {
+__global__ __launch_bounds__(256) void ew_kernel(const void* x, int xdt, int64_t ldx, void* __restrict__ y,
+                                                 int ydt, int64_t ldy, const float* __restrict__ gamma, int M, int N,
+                                                 const float* src = nullptr, int64_t lds = 0) {
   const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   const int64_t nvec = (int64_t)M * N;
   if (i >= nvec) return;
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(256) void ew_kernel(const void* __restrict__ x, int
     float br[4], acc[4];
     load4(y, ydt, (int64_t)r * ldy + c, br);
     float* xp = (float*)x + (int64_t)r * ldx + c;
-    const f4 xv = *(const f4*)xp;
+    const f4 xv = *(const f4*)(src + (int64_t)r * lds + c);
     const f4 gv = *(const f4*)(gamma + c);
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[j] = xv[j] + gv[j] * br[j];
@@ -738,15 +739,22 @@ extern "C" int vggt_gelu_bwd(const void* dh, int dhdtype, int64_t lddh, const vo
   return VGGT_OK;
 }
 
-extern "C" int vggt_resid_scale_add(float* x, int64_t ldx, const void* branch, int bdtype, int64_t ldb,
-                                    const float* gamma, int M, int N, void* stream) {
+extern "C" int vggt_resid_scale_add_from(float* out, int64_t ldo, const float* x, int64_t ldx, const void* branch,
+                                         int bdtype, int64_t ldb, const float* gamma, int M, int N, void* stream) {
   if (M <= 0 || N <= 0 || N % 4) return M == 0 ? VGGT_OK : VGGT_ERR_SHAPE;
-  if ((ldx | ldb) % 4 || (uintptr_t)x % 16 || (uintptr_t)gamma % 16 || (uintptr_t)branch % 8) return VGGT_ERR_ALIGN;
+  if ((ldo | ldx | ldb) % 4 || (uintptr_t)out % 16 || (uintptr_t)x % 16 || (uintptr_t)gamma % 16 ||
+      (uintptr_t)branch % 8)
+    return VGGT_ERR_ALIGN;
   const int64_t nv = (int64_t)M * N / 4;
-  ew_kernel<1><<<(unsigned)((nv + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, VGGT_DTYPE_F32, ldx, (void*)branch,
-                                                                               bdtype, ldb, gamma, M, N);
+  ew_kernel<1><<<(unsigned)((nv + 255) / 256), 256, 0, (hipStream_t)stream>>>(out, VGGT_DTYPE_F32, ldo, (void*)branch,
+                                                                               bdtype, ldb, gamma, M, N, x, ldx);
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
+}
+
+extern "C" int vggt_resid_scale_add(float* x, int64_t ldx, const void* branch, int bdtype, int64_t ldb,
+                                    const float* gamma, int M, int N, void* stream) {
+  return vggt_resid_scale_add_from(x, ldx, x, ldx, branch, bdtype, ldb, gamma, M, N, stream);
 }
 
 extern "C" int vggt_transpose_b16(const void* src, int64_t lds, int rows, int cols, void* dst, int64_t ldd,

@@ -153,6 +153,72 @@ def test_headnorm_rope(N, D, mode):
     assert torch.equal(buf[:, :1024].cpu(), qkv[:, :1024])
 
 
+@pytest.mark.parametrize("D,mode", [(64, 1), (128, 2), (64, 0)])
+def test_norm_rope_out_of_place_matches_in_place(N, D, mode):
+    """vggt_qknorm_rope_out / vggt_headnorm_rope_out (training recompute) are
+    bit-identical to the in-place forms and leave the source untouched."""
+    from aligned_vggt.backbone.layers import RopeTables
+    H, M = 1024 // D, 3 * 21
+    g = torch.Generator().manual_seed(7 + D + mode)
+    src = (torch.randn(M, 3 * 1024, generator=g) * 2).to(torch.bfloat16).cuda()
+    qw, qb, kw, kb = (torch.randn(D, generator=g).cuda() for _ in range(4))
+    rt, period = None, 1
+    if mode == 1:
+        pos = O.position_grid(1, 4, 4, 5)[0]
+        rt, period = RopeTables(pos, D, 100.0, "cuda"), pos.shape[0]
+    elif mode == 2:
+        pos = torch.randint(0, 30, (7,), generator=g)
+        rt, period = RopeTables(pos, D, 100.0, "cuda", mode=2), 7
+    tabs = (rt.pos, period, rt.cos, rt.sin) if rt else (None, 1, None, None)
+    keep = src.clone()
+    inplace = src.clone()
+    N.qknorm_rope(inplace, H, D, qw, qb, kw, kb, 1e-5, mode, *tabs)
+    dst = torch.zeros(M, 2 * 1024, device="cuda", dtype=torch.bfloat16)
+    N.qknorm_rope_out(src, dst, H, D, qw, qb, kw, kb, 1e-5, mode, *tabs)
+    assert torch.equal(dst, inplace[:, :2048])
+    assert torch.equal(src, keep)
+    inplace = src.clone()
+    N.headnorm_rope(inplace, 1024, H, D, kw, kb, 1e-5, mode, *tabs)
+    dst = torch.zeros(M, 1024, device="cuda", dtype=torch.bfloat16)
+    N.headnorm_rope_out(src[:, 1024:], dst, H, D, kw, kb, 1e-5, mode, *tabs)
+    assert torch.equal(dst, inplace[:, 1024:2048])
+    assert torch.equal(src, keep)
+
+
+def test_gemm_gelu_pre(N):
+    """vggt_gemm_bf16_gelu_pre = the plain GEMM (pre) and the GELU epilogue (out), both bit-identical to the
+    separate launches, on the 128x128 (small M) and ping-pong (M >= 4096) forms."""
+    g = torch.Generator(device="cuda").manual_seed(11)
+    for M in (300, 4200):
+        a = (torch.randn(M, 1024, device="cuda", generator=g)).to(torch.bfloat16)
+        w = (torch.randn(4096, 1024, device="cuda", generator=g) * 0.03).to(torch.bfloat16)
+        b = torch.randn(4096, device="cuda", generator=g) * 0.1
+        out = torch.empty(M, 4096, device="cuda", dtype=torch.bfloat16)
+        pre = torch.empty_like(out)
+        N.gemm_bf16_gelu_pre(a, w, b, out, pre)
+        ref_pre = torch.empty_like(out)
+        N.gemm_bf16(a, w, b, ref_pre, N.EPI_BF16)
+        ref_out = torch.empty_like(out)
+        N.gemm_bf16(a, w, b, ref_out, N.EPI_GELU_BF16)
+        assert torch.equal(pre, ref_pre)
+        assert torch.equal(out, ref_out)
+        assert _rel(out, F.gelu(ref_pre.float())) < 4e-3
+
+
+def test_resid_scale_add_from(N):
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randn(77, 1024, device="cuda", generator=g)
+    br = torch.randn(77, 1024, device="cuda", generator=g).to(torch.bfloat16)
+    gamma = torch.rand(1024, device="cuda", generator=g)
+    out = torch.empty_like(x)
+    keep = x.clone()
+    N.resid_scale_add_from(out, x, br, gamma)
+    assert torch.equal(x, keep)
+    assert torch.allclose(out, x + gamma * br.float(), rtol=1e-6, atol=1e-6)
+    N.resid_scale_add(x, br, gamma)
+    assert torch.equal(x, out)
+
+
 def _ref_attn(q, k, v, scale):
     s = (q.float() @ k.float().transpose(-1, -2)) * scale
     return torch.softmax(s, -1) @ v.float()
