@@ -19,7 +19,7 @@
 //    dP = dO V^T (key on the lane), then dV^T += dO^T P and dK^T += Q^T dS
 //    with transposed reads of the Q / dO tiles.
 // LDS rows are padded by 16 B (no swizzle: every tile is read both by rows
-// and transposed); tiles are staged global -> VGPR -> LDS.
+// and transposed); tiles are staged global -> VGPR -> LDS, double-buffered.
 #include <math.h>
 
 #include "common.h"
@@ -40,13 +40,41 @@ struct BwdArgs {
   float scale, c;
 };
 
+// Register-prefetched staging: tile t+1 is loaded into VGPRs before tile t's
+// MFMAs and written to the other LDS buffer after them.
+template <int D, int NR>
+struct TilePrefetch {  // NR rows x D of a bf16 operand, spread over 256 threads
+  static constexpr int CPR = D / 8, PER = NR * CPR / 256;
+  uint4 v[PER];
+  __device__ __forceinline__ void load(const bf16_t* src, int64_t ld, int r0, int valid) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int idx = threadIdx.x + 256 * i, row = idx / CPR, ch = idx % CPR;
+      const int r = r0 + row;
+      v[i] = r < valid ? *(const uint4*)(src + (int64_t)r * ld + ch * 8) : uint4{0u, 0u, 0u, 0u};
+    }
+  }
+  __device__ __forceinline__ void store(char* tile) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int idx = threadIdx.x + 256 * i, row = idx / CPR, ch = idx % CPR;
+      *(uint4*)(tile + row * Geo<D>::ROWP + ch * 16) = v[i];
+    }
+  }
+};
+
 // ------------------------------------------------------------------ dQ
 template <int D>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(BwdArgs a) {
+constexpr size_t dq_lds_bytes() {
+  return (size_t)2 * 2 * 64 * Geo<D>::ROWP;
+}
+
+template <int D>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(BwdArgs a) {
   using G = Geo<D>;
   constexpr int BK = 64;
   constexpr int TILEB = BK * G::ROWP;
-  __shared__ __attribute__((aligned(16))) char smem[2 * TILEB];
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [buf][K | V][64][ROWP]
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int hl = lane >> 5;
@@ -81,18 +109,26 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(BwdArgs a) {
 #pragma unroll
   for (int i = 0; i < G::NDB; ++i) dq[i] = f32x16{};
   const int nt = (a.nk + BK - 1) / BK;
+  TilePrefetch<D, BK> pk, pv;
+  pk.load(kp, a.ldk, 0, a.nk);
+  pv.load(vp, a.ldv, 0, a.nk);
+  pk.store(smem);
+  pv.store(smem + TILEB);
+  __syncthreads();
   for (int t = 0; t < nt; ++t) {
-    __syncthreads();
-    stage_rows<D>(smem, kp, a.ldk, t * BK, BK, a.nk);
-    stage_rows<D>(smem + TILEB, vp, a.ldv, t * BK, BK, a.nk);
-    __syncthreads();
+    const char* sk = smem + (t & 1) * 2 * TILEB;
+    const char* sv = sk + TILEB;
+    if (t + 1 < nt) {
+      pk.load(kp, a.ldk, (t + 1) * BK, a.nk);
+      pv.load(vp, a.ldv, (t + 1) * BK, a.nk);
+    }
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
       f32x16 st = f32x16{}, dpt = f32x16{};
 #pragma unroll
       for (int ks = 0; ks < G::NKS; ++ks) {
-        st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag<D>(smem, kb * 32, ks, lane), qf[ks], st, 0, 0, 0);
-        dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag<D>(smem + TILEB, kb * 32, ks, lane), gf[ks], dpt, 0, 0, 0);
+        st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag<D>(sk, kb * 32, ks, lane), qf[ks], st, 0, 0, 0);
+        dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag<D>(sv, kb * 32, ks, lane), gf[ks], dpt, 0, 0, 0);
       }
       f32x16 ds;
 #pragma unroll
@@ -106,9 +142,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(BwdArgs a) {
         const bf16x8 dsf = pack8(ds, ss);
 #pragma unroll
         for (int db = 0; db < G::NDB; ++db)
-          dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag<D>(smem, db, kb, ss, lane), dsf, dq[db], 0, 0, 0);
+          dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag<D>(sk, db, kb, ss, lane), dsf, dq[db], 0, 0, 0);
       }
     }
+    if (t + 1 < nt) {
+      char* nb = smem + ((t + 1) & 1) * 2 * TILEB;
+      pk.store(nb);
+      pv.store(nb + TILEB);
+    }
+    __syncthreads();
   }
   if (qrow < a.nq) {
     bf16_t* dp = a.dq + ((int64_t)b * a.qbs + qrow) * a.lddq + h * D;
@@ -125,18 +167,26 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(BwdArgs a) {
 }
 
 // ------------------------------------------------------------------ dK, dV
+// A wave owns 32 keys: its K rows live in registers as the B operand of
+// S = Q K^T (loaded once), the workgroup's 128 V rows in LDS (B operand of
+// dP = dO V^T).  The 32-query Q / dO tiles and their lse / delta are
+// double-buffered: tile t+1 is loaded into registers before tile t's MFMAs
+// and written to the other LDS buffer after them, one barrier per tile.
+// 70 KB of LDS -> two workgroups per CU.
 template <int D>
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(BwdArgs a) {
+constexpr size_t dkdv_lds_bytes() {
+  return (size_t)128 * Geo<D>::ROWP + (size_t)2 * 2 * 32 * Geo<D>::ROWP + 2 * 2 * 32 * 4;
+}
+
+template <int D>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(BwdArgs a) {
   using G = Geo<D>;
   constexpr int BKEY = 128, BQT = 32;
-  constexpr int KVB = BKEY * G::ROWP, QTB = BQT * G::ROWP;
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2*KVB + 2*QTB + 2*BQT*4 bytes
-  char* sk = smem;
-  char* sv = smem + KVB;
-  char* sq = smem + 2 * KVB;
-  char* sg = sq + QTB;
-  float* slse = (float*)(sg + QTB);
-  float* sdel = slse + BQT;
+  constexpr int QTB = BQT * G::ROWP;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* sv = smem;                                  // V rows of the block [128][ROWP]
+  char* sqg = smem + BKEY * G::ROWP;                // [buf][Q | dO][32][ROWP]
+  float* sld = (float*)(sqg + 4 * QTB);             // [buf][lse | delta][32]
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int hl = lane >> 5;
@@ -150,27 +200,48 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(BwdArgs a) {
   const bf16_t* gp = a.dout + (int64_t)b * a.obs * a.ldo + h * D;
   const int64_t rbase = ((int64_t)b * a.heads + h) * a.nq;
 
-  stage_rows<D>(sk, kp, a.ldk, kb0 * BKEY, BKEY, a.nk);
+  // this wave's K rows (B operand of S = Q K^T: column = key)
+  const int krow = kb0 * BKEY + wave * 32 + (lane & 31);
+  const int kr = min(krow, a.nk - 1);
+  bf16x8 kf[G::NKS];
+#pragma unroll
+  for (int ks = 0; ks < G::NKS; ++ks) kf[ks] = *(const bf16x8*)(kp + (int64_t)kr * a.ldk + ks * 16 + 8 * hl);
   stage_rows<D>(sv, vp, a.ldv, kb0 * BKEY, BKEY, a.nk);
+
+  TilePrefetch<D, 32> pq, pg;
+  float pls = 0.f;
+  auto load_tile = [&](int t) {
+    pq.load(qp, a.ldq, t * BQT, a.nq);
+    pg.load(gp, a.ldo, t * BQT, a.nq);
+    if (threadIdx.x < 2 * BQT) {
+      const int qq = t * BQT + (threadIdx.x & (BQT - 1));
+      pls = threadIdx.x < BQT ? (qq < a.nq ? a.lse[rbase + qq] : INFINITY) : (qq < a.nq ? a.delta[rbase + qq] : 0.f);
+    }
+  };
+  auto store_tile = [&](int buf) {
+    pq.store(sqg + (2 * buf) * QTB);
+    pg.store(sqg + (2 * buf + 1) * QTB);
+    if (threadIdx.x < 2 * BQT) sld[buf * 2 * BQT + threadIdx.x] = pls;
+  };
+
   f32x16 dk[G::NDB], dv[G::NDB];
 #pragma unroll
   for (int i = 0; i < G::NDB; ++i) dk[i] = dv[i] = f32x16{};
   const int nt = (a.nq + BQT - 1) / BQT;
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
   for (int t = 0; t < nt; ++t) {
-    __syncthreads();
-    stage_rows<D>(sq, qp, a.ldq, t * BQT, BQT, a.nq);
-    stage_rows<D>(sg, gp, a.ldo, t * BQT, BQT, a.nq);
-    if (threadIdx.x < BQT) {
-      const int qq = t * BQT + threadIdx.x;
-      slse[threadIdx.x] = qq < a.nq ? a.lse[rbase + qq] : INFINITY;
-      sdel[threadIdx.x] = qq < a.nq ? a.delta[rbase + qq] : 0.f;
-    }
-    __syncthreads();
+    const int buf = t & 1;
+    if (t + 1 < nt) load_tile(t + 1);
+    const char* sq = sqg + (2 * buf) * QTB;
+    const char* sg = sqg + (2 * buf + 1) * QTB;
+    const float* slse = sld + buf * 2 * BQT;
+    const float* sdel = slse + BQT;
     f32x16 s = f32x16{}, dp = f32x16{};
 #pragma unroll
     for (int ks = 0; ks < G::NKS; ++ks) {
-      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag<D>(sq, 0, ks, lane), rowfrag<D>(sk, wave * 32, ks, lane), s,
-                                                  0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag<D>(sq, 0, ks, lane), kf[ks], s, 0, 0, 0);
       dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rowfrag<D>(sg, 0, ks, lane), rowfrag<D>(sv, wave * 32, ks, lane),
                                                    dp, 0, 0, 0);
     }
@@ -191,8 +262,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(BwdArgs a) {
         dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag<D>(sq, db, 0, ss, lane), dsf, dk[db], 0, 0, 0);
       }
     }
+    if (t + 1 < nt) store_tile(buf ^ 1);
+    __syncthreads();
   }
-  const int krow = kb0 * BKEY + wave * 32 + (lane & 31);
   if (krow < a.nk) {
     bf16_t* kq = a.dk + ((int64_t)b * a.kbs + krow) * a.lddkv + h * D;
     bf16_t* vq = a.dv + ((int64_t)b * a.kbs + krow) * a.lddkv + h * D;
@@ -231,21 +303,24 @@ extern "C" int vggt_attention_bwd(const void* q, int64_t ldq, int64_t q_bstride,
   hipStream_t s = (hipStream_t)stream;
   const int g1 = ((nq + 127) / 128) * heads * batch;
   const int g2 = ((nk + 127) / 128) * heads * batch;
-  auto lds_kv = [](int DD) { return (size_t)2 * 128 * (DD * 2 + 16) + (size_t)2 * 32 * (DD * 2 + 16) + 2 * 32 * 4; };
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds_kv(64));
+                              (int)dkdv_lds_bytes<64>());
     (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds_kv(128));
+                              (int)dkdv_lds_bytes<128>());
+    (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)dq_lds_bytes<64>());
+    (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)dq_lds_bytes<128>());
     attr_set = true;
   }
   if (D == 64) {
-    attn_bwd_dq_kernel<64><<<g1, 256, 0, s>>>(a);
-    attn_bwd_dkdv_kernel<64><<<g2, 256, lds_kv(64), s>>>(a);
+    attn_bwd_dq_kernel<64><<<g1, 256, dq_lds_bytes<64>(), s>>>(a);
+    attn_bwd_dkdv_kernel<64><<<g2, 256, dkdv_lds_bytes<64>(), s>>>(a);
   } else {
-    attn_bwd_dq_kernel<128><<<g1, 256, 0, s>>>(a);
-    attn_bwd_dkdv_kernel<128><<<g2, 256, lds_kv(128), s>>>(a);
+    attn_bwd_dq_kernel<128><<<g1, 256, dq_lds_bytes<128>(), s>>>(a);
+    attn_bwd_dkdv_kernel<128><<<g2, 256, dkdv_lds_bytes<128>(), s>>>(a);
   }
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
