@@ -102,6 +102,7 @@ __global__ __launch_bounds__(256) void colred_kernel(const void* __restrict__ a,
     g[2] = gv[2];
     g[3] = gv[3];
   }
+#pragma unroll 4
   for (int r = r0; r < r1; ++r) {
     float av[4];
     load4(a, adt, (int64_t)r * lda + c0, av);
@@ -232,12 +233,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ x,
     const int gi = r / rm.G, ii = r % rm.G;
     const int64_t xr = (int64_t)gi * rm.xgs + rm.xoff + ii;
     const int64_t yr = (int64_t)gi * rm.ygs + rm.yoff + ii;
-    float v[NV][4], g[NV][4];
+    float v[NV][4], g[NV][4], prev[NV][4];
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = i * 256 + lane * 4;
       load4(x, xdt, xr * ldx + c, v[i]);
       load4(dy, ydt, yr * ldy + c, g[i]);
+      if (accumulate) load4(dx, dxdt, xr * lddx + c, prev[i]);  // issued with the operands, used at the end
     }
     float s = 0.f;
 #pragma unroll
@@ -276,10 +278,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ x,
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = rstd * (g[i][j] - m1 - v[i][j] * m2);
       if (accumulate) {
-        float prev[4];
-        load4(dx, dxdt, xr * lddx + c, prev);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] += prev[j];
+        for (int j = 0; j < 4; ++j) o[j] += prev[i][j];
       }
       store4(dx, dxdt, xr * lddx + c, o);
     }
@@ -664,16 +664,21 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   *o = accumulate ? *o + s : s;
 }
 
-int nchunks_for(int M, int maxc) {
-  int c = (M + 63) / 64;
+int nchunks_for(int M, int maxc, int rows = 64) {
+  int c = (M + rows - 1) / rows;
   return c < 1 ? 1 : (c > maxc ? maxc : c);
 }
+// Row chunking of the column reductions / row-wise backward kernels: enough
+// workgroups (up to ~4 per CU) that the serial per-row loads of each wave
+// overlap across waves; more chunks only add fp32 partials (<= 8 MB).
+constexpr int COLRED_MAXC = 1024, COLRED_ROWS = 16;
+constexpr int ROWBWD_MAXC = 2048, ROWBWD_ROWS = 16;
 
 }  // namespace
 
 // ============================================================ C ABI
 extern "C" size_t vggt_colred_workspace_bytes(int M, int N) {
-  return (size_t)2 * nchunks_for(M, 256) * (size_t)N * sizeof(float);
+  return (size_t)2 * nchunks_for(M, COLRED_MAXC, COLRED_ROWS) * (size_t)N * sizeof(float);
 }
 
 extern "C" int vggt_colsum(const void* x, int dtype, int64_t ldx, int M, int N, float* out, int accumulate, void* ws,
@@ -681,7 +686,7 @@ extern "C" int vggt_colsum(const void* x, int dtype, int64_t ldx, int M, int N, 
   if (M <= 0 || N <= 0 || N % 4) return VGGT_ERR_SHAPE;
   if (dtype != VGGT_DTYPE_F32 && dtype != VGGT_DTYPE_BF16) return VGGT_ERR_UNSUPPORTED;
   if (ldx % 4 || (uintptr_t)x % 8) return VGGT_ERR_ALIGN;
-  const int nc = nchunks_for(M, 256);
+  const int nc = nchunks_for(M, COLRED_MAXC, COLRED_ROWS);
   if (!ws || ws_bytes < (size_t)nc * N * sizeof(float)) return VGGT_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
   const int rpc = (M + nc - 1) / nc;
@@ -698,7 +703,7 @@ extern "C" int vggt_layerscale_bwd(const float* dout, int64_t ldd, const void* b
   if (M <= 0 || N <= 0 || N % 4) return VGGT_ERR_SHAPE;
   if ((ldd | ldb | ldo) % 4 || ((uintptr_t)dout | (uintptr_t)gamma) % 16 || ((uintptr_t)branch | (uintptr_t)dbranch) % 8)
     return VGGT_ERR_ALIGN;
-  const int nc = nchunks_for(M, 256);
+  const int nc = nchunks_for(M, COLRED_MAXC, COLRED_ROWS);
   if (!ws || ws_bytes < (size_t)2 * nc * N * sizeof(float)) return VGGT_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
   const int rpc = (M + nc - 1) / nc;
@@ -727,7 +732,7 @@ extern "C" int vggt_gelu_bwd(const void* dh, int dhdtype, int64_t lddh, const vo
                              size_t ws_bytes, void* stream) {
   if (M <= 0 || N <= 0 || N % 4) return VGGT_ERR_SHAPE;
   if ((lddh | ldp | ldo) % 4 || ((uintptr_t)dh | (uintptr_t)pre | (uintptr_t)dpre) % 8) return VGGT_ERR_ALIGN;
-  const int nc = nchunks_for(M, 256);
+  const int nc = nchunks_for(M, COLRED_MAXC, COLRED_ROWS);
   if (!ws || ws_bytes < (size_t)nc * N * sizeof(float)) return VGGT_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
   const int rpc = (M + nc - 1) / nc;
@@ -769,7 +774,7 @@ extern "C" int vggt_transpose_b16(const void* src, int64_t lds, int rows, int co
 }
 
 extern "C" size_t vggt_layernorm_bwd_workspace_bytes(int M, int C) {
-  return (size_t)2 * nchunks_for(M, 512) * (size_t)C * sizeof(float);
+  return (size_t)2 * nchunks_for(M, ROWBWD_MAXC, ROWBWD_ROWS) * (size_t)C * sizeof(float);
 }
 
 extern "C" int vggt_layernorm_bwd(const void* x, int xdtype, int64_t ldx, const float* w, float eps, const void* dy,
@@ -780,7 +785,7 @@ extern "C" int vggt_layernorm_bwd(const void* x, int xdtype, int64_t ldx, const 
   if (C % 256 || C > 1024 || group <= 0) return VGGT_ERR_SHAPE;
   if (accumulate && dxdtype != VGGT_DTYPE_F32) return VGGT_ERR_UNSUPPORTED;
   if ((ldx | ldy | lddx) % 4 || ((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx) % 8) return VGGT_ERR_ALIGN;
-  const int nblk = nchunks_for(M, 512);
+  const int nblk = nchunks_for(M, ROWBWD_MAXC, ROWBWD_ROWS);
   const bool want = dw || db;
   if (want && (!ws || ws_bytes < (size_t)2 * nblk * C * sizeof(float))) return VGGT_ERR_SHAPE;
   const int rpb = (M + nblk - 1) / nblk;
@@ -800,7 +805,7 @@ extern "C" int vggt_layernorm_bwd(const void* x, int xdtype, int64_t ldx, const 
 }
 
 extern "C" size_t vggt_headnorm_rope_bwd_workspace_bytes(int M, int D) {
-  return (size_t)4 * nchunks_for(M, 512) * (size_t)D * sizeof(float);
+  return (size_t)4 * nchunks_for(M, ROWBWD_MAXC, ROWBWD_ROWS) * (size_t)D * sizeof(float);
 }
 
 extern "C" int vggt_headnorm_rope_bwd(const void* pre, int64_t ldp, void* grad, int64_t ldg, int dtype, int M, int H,
@@ -814,7 +819,7 @@ extern "C" int vggt_headnorm_rope_bwd(const void* pre, int64_t ldp, void* grad, 
   if ((ldp | ldg) % 8 || ((uintptr_t)pre | (uintptr_t)grad) % 16) return VGGT_ERR_ALIGN;
   if (rope_mode != VGGT_ROPE_NONE && (!pos || !cos_tab || !sin_tab || period <= 0 || tab_len <= 0))
     return VGGT_ERR_SHAPE;
-  const int nblk = nchunks_for(M, 512);
+  const int nblk = nchunks_for(M, ROWBWD_MAXC, ROWBWD_ROWS);
   const bool want = (w0 || w1) && (dw0 || db0 || dw1 || db1);
   if (want && (!ws || ws_bytes < (size_t)4 * nblk * D * sizeof(float))) return VGGT_ERR_SHAPE;
   const int rpb = (M + nblk - 1) / nblk;
