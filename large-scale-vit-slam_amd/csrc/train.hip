@@ -451,46 +451,83 @@ __global__ __launch_bounds__(256) void headnorm_rope_bwd_kernel(const void* __re
 // recompute S = q k^T * scale, P = softmax(S); dP = dO v^T;
 // dS = P * (dP - rowsum(P * dP)); dq = scale dS k; dk = scale dS^T q; dv = P^T dO.
 // (rowsum(P * dP) = rowsum(dO * O): the same delta without reading O.)
+// Operand rows are padded to D+1 floats so the score loops (a thread per
+// (query, key), key rows at stride D+1) are bank-conflict free; operands are
+// read 16 B per lane when rows are 16-B aligned (vec), and each thread of the
+// output loops produces two adjacent columns (one 4-B bf16x2 / 8-B f32x2 store).
 __global__ __launch_bounds__(256) void attn_small_bwd_kernel(
     const void* __restrict__ q, int64_t ldq, int64_t qbs, const void* __restrict__ k, int64_t ldk, int64_t kbs,
     const void* __restrict__ v, int64_t ldv, int64_t vbs, const void* __restrict__ dout, int64_t ldo, int64_t obs,
     void* __restrict__ dq, int64_t ldgq, int64_t gqbs, void* __restrict__ dk, void* __restrict__ dv, int64_t ldgk,
-    int64_t gkbs, int dtype, int heads, int nq, int nk, int D, float scale) {
+    int64_t gkbs, int dtype, int heads, int nq, int nk, int D, float scale, int vec) {
   extern __shared__ float sm[];
-  float* sq = sm;                 // [nq][D]
-  float* sdo = sq + nq * D;       // [nq][D]
-  float* sk = sdo + nq * D;       // [nk][D]
-  float* sv = sk + nk * D;        // [nk][D]
-  float* sp = sv + nk * D;        // [nq][nk]  P, then dS
-  float* sdp = sp + nq * nk;      // [nq][nk]  dP
-  const int lane = threadIdx.x;
+  const int DP = D + 1;
+  float* sq = sm;                 // [nq][DP]
+  float* sdo = sq + nq * DP;      // [nq][DP]
+  float* sk = sdo + nq * DP;      // [nk][DP]
+  float* sv = sk + nk * DP;       // [nk][DP]
+  float* sp = sv + nk * DP;       // [nq][nk]  P, then dS
+  float* sdp = sp + nq * nk;      // [nq][nk]  dP, then P
+  const int tid = threadIdx.x;
   const int b = blockIdx.x / heads, h = blockIdx.x % heads;
-  auto ld1 = [&](const void* base, int64_t off) -> float {
-    return dtype == VGGT_DTYPE_BF16 ? bf2f(((const bf16_t*)base)[off]) : ((const float*)base)[off];
-  };
-  for (int i = lane; i < nq * D; i += 256) {
-    const int r = i / D, c = i % D;
-    sq[i] = ld1(q, ((int64_t)b * qbs + r) * ldq + h * D + c);
-    sdo[i] = ld1(dout, ((int64_t)b * obs + r) * ldo + h * D + c);
-  }
-  for (int i = lane; i < nk * D; i += 256) {
-    const int r = i / D, c = i % D;
-    sk[i] = ld1(k, ((int64_t)b * kbs + r) * ldk + h * D + c);
-    sv[i] = ld1(v, ((int64_t)b * kbs + r) * ldv + h * D + c);
-  }
-  __syncthreads();
-  for (int i = lane; i < nq * nk; i += 256) {
-    const int r = i / nk, c = i % nk;
-    float s = 0.f, t = 0.f;
-    for (int d = 0; d < D; ++d) {
-      s += sq[r * D + d] * sk[c * D + d];
-      t += sdo[r * D + d] * sv[c * D + d];
+  const bool bf = dtype == VGGT_DTYPE_BF16;
+  auto stage = [&](float* dst, const void* base, int64_t bs, int64_t ld, int rows) {
+    if (vec) {
+      const int cpr = D / 8;
+      for (int i = tid; i < rows * cpr; i += 256) {
+        const int r = i / cpr, ch = i % cpr;
+        const int64_t off = ((int64_t)b * bs + r) * ld + h * D + ch * 8;
+        float f[8];
+        if (bf) {
+          const uint4 u = *(const uint4*)((const bf16_t*)base + off);
+          const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            f[2 * t] = bf2f((bf16_t)(w4[t] & 0xffff));
+            f[2 * t + 1] = bf2f((bf16_t)(w4[t] >> 16));
+          }
+        } else {
+          const f4 a0 = *(const f4*)((const float*)base + off), a1 = *(const f4*)((const float*)base + off + 4);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            f[t] = a0[t];
+            f[4 + t] = a1[t];
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) dst[r * DP + ch * 8 + t] = f[t];
+      }
+    } else {
+      for (int i = tid; i < rows * D; i += 256) {
+        const int r = i / D, c = i % D;
+        const int64_t off = ((int64_t)b * bs + r) * ld + h * D + c;
+        dst[r * DP + c] = bf ? bf2f(((const bf16_t*)base)[off]) : ((const float*)base)[off];
+      }
     }
-    sp[i] = s * scale;
-    sdp[i] = t;
+  };
+  stage(sq, q, qbs, ldq, nq);
+  stage(sdo, dout, obs, ldo, nq);
+  stage(sk, k, kbs, ldk, nk);
+  stage(sv, v, vbs, ldv, nk);
+  __syncthreads();
+  for (int i = tid; i < nq * nk; i += 256) {
+    const int r = i / nk, c = i % nk;
+    const float* qr = sq + r * DP;
+    const float* gr = sdo + r * DP;
+    const float* kr = sk + c * DP;
+    const float* vr = sv + c * DP;
+    float s0 = 0.f, s1 = 0.f, t0 = 0.f, t1 = 0.f;
+    for (int d = 0; d < D; d += 2) {
+      s0 += qr[d] * kr[d];
+      s1 += qr[d + 1] * kr[d + 1];
+      t0 += gr[d] * vr[d];
+      t1 += gr[d + 1] * vr[d + 1];
+    }
+    sp[i] = (s0 + s1) * scale;
+    sdp[i] = t0 + t1;
   }
   __syncthreads();
-  for (int r = lane; r < nq; r += 256) {
+  for (int r = tid; r < nq; r += 256) {
     float m = -INFINITY;
     for (int c = 0; c < nk; ++c) m = fmaxf(m, sp[r * nk + c]);
     float l = 0.f;
@@ -514,25 +551,37 @@ __global__ __launch_bounds__(256) void attn_small_bwd_kernel(
     }
   }
   __syncthreads();
-  auto st1 = [&](void* base, int64_t off, float val) {
-    if (dtype == VGGT_DTYPE_BF16) ((bf16_t*)base)[off] = f2bf(val);
-    else ((float*)base)[off] = val;
-  };
-  for (int i = lane; i < nq * D; i += 256) {
-    const int r = i / D, c = i % D;
-    float s = 0.f;
-    for (int j = 0; j < nk; ++j) s += sp[r * nk + j] * sk[j * D + c];
-    st1(dq, ((int64_t)b * gqbs + r) * ldgq + h * D + c, s * scale);
-  }
-  for (int i = lane; i < nk * D; i += 256) {
-    const int r = i / D, c = i % D;
-    float s = 0.f, t = 0.f;
-    for (int j = 0; j < nq; ++j) {
-      s += sp[j * nk + r] * sq[j * D + c];
-      t += sdp[j * nk + r] * sdo[j * D + c];
+  auto st2 = [&](void* base, int64_t off, float a0, float a1) {
+    if (bf) {
+      *(uint32_t*)((bf16_t*)base + off) = pack_bf2(a0, a1);
+    } else {
+      ((float*)base)[off] = a0;
+      ((float*)base)[off + 1] = a1;
     }
-    st1(dk, ((int64_t)b * gkbs + r) * ldgk + h * D + c, s * scale);
-    st1(dv, ((int64_t)b * gkbs + r) * ldgk + h * D + c, t);
+  };
+  const int D2 = D / 2;
+  for (int i = tid; i < nq * D2; i += 256) {
+    const int r = i / D2, c = 2 * (i % D2);
+    float s0 = 0.f, s1 = 0.f;
+    for (int j = 0; j < nk; ++j) {
+      const float ds = sp[r * nk + j];
+      s0 += ds * sk[j * DP + c];
+      s1 += ds * sk[j * DP + c + 1];
+    }
+    st2(dq, ((int64_t)b * gqbs + r) * ldgq + h * D + c, s0 * scale, s1 * scale);
+  }
+  for (int i = tid; i < nk * D2; i += 256) {
+    const int r = i / D2, c = 2 * (i % D2);
+    float s0 = 0.f, s1 = 0.f, t0 = 0.f, t1 = 0.f;
+    for (int j = 0; j < nq; ++j) {
+      const float ds = sp[j * nk + r], p = sdp[j * nk + r];
+      s0 += ds * sq[j * DP + c];
+      s1 += ds * sq[j * DP + c + 1];
+      t0 += p * sdo[j * DP + c];
+      t1 += p * sdo[j * DP + c + 1];
+    }
+    st2(dk, ((int64_t)b * gkbs + r) * ldgk + h * D + c, s0 * scale, s1 * scale);
+    st2(dv, ((int64_t)b * gkbs + r) * ldgk + h * D + c, t0, t1);
   }
 }
 
@@ -859,11 +908,20 @@ extern "C" int vggt_attention_small_bwd(const void* q, int64_t ldq, int64_t q_bs
                                         int nq, int nk, int D, float scale, void* stream) {
   if (batch <= 0 || heads <= 0 || nq <= 0 || nk <= 0 || D <= 0) return VGGT_ERR_SHAPE;
   if (dtype != VGGT_DTYPE_F32 && dtype != VGGT_DTYPE_BF16) return VGGT_ERR_UNSUPPORTED;
-  const size_t lds = ((size_t)2 * nq * D + (size_t)2 * nk * D + (size_t)2 * nq * nk) * sizeof(float);
+  if (D % 2) return VGGT_ERR_SHAPE;
+  const int esz = dtype == VGGT_DTYPE_BF16 ? 2 : 4;
+  // two adjacent output columns per store: 4-B (bf16x2) / 4-B-aligned f32 pairs
+  if ((lddq | lddkv) % 2 || ((uintptr_t)dq | (uintptr_t)dk | (uintptr_t)dv) % (2 * esz > 4 ? 4 : 2 * esz))
+    return VGGT_ERR_ALIGN;
+  const size_t lds = ((size_t)2 * nq * (D + 1) + (size_t)2 * nk * (D + 1) + (size_t)2 * nq * nk) * sizeof(float);
   if (lds > 64 * 1024) return VGGT_ERR_SHAPE;
+  // 16-B operand reads when every row start of every operand is 16-B aligned
+  const int64_t al = 16 / esz;
+  const int vec = D % 8 == 0 && (ldq | ldk | ldv | ldo) % al == 0 &&
+                  ((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)dout) % 16 == 0;
   attn_small_bwd_kernel<<<batch * heads, 256, lds, (hipStream_t)stream>>>(
       q, ldq, q_bstride, k, ldk, k_bstride, v, ldv, k_bstride, dout, ldo, o_bstride, dq, lddq, dq_bstride, dk, dv,
-      lddkv, dkv_bstride, dtype, heads, nq, nk, D, scale);
+      lddkv, dkv_bstride, dtype, heads, nq, nk, D, scale, vec);
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
 }
