@@ -143,11 +143,16 @@ __device__ __forceinline__ void write_tile(const char* Cs, int m0, int n0, int M
         int pp = two_d ? ep.pos[2 * pr + (e0 >= D / 2 ? 1 : 0)] : ep.pos[pr];
         pp = min(max(pp, 0), ep.tab_len - 1);
         const bool first = er < RD / 2;
+        const f32x4* cp = (const f32x4*)(tcs + pp * RD + er);  // 32-B aligned: two 16-B reads each
+        const f32x4* sp = (const f32x4*)(tsn + pp * RD + er);
+        const f32x4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
+        const float cv[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+        const float sv[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
         float y[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float partner = __shfl_xor(x[j], PL, 64);
-          y[j] = x[j] * tcs[pp * RD + er + j] + (first ? -partner : partner) * tsn[pp * RD + er + j];
+          y[j] = x[j] * cv[j] + (first ? -partner : partner) * sv[j];
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) x[j] = y[j];
@@ -885,7 +890,7 @@ extern "C" int vggt_gemm_qkv(const void* A, int64_t lda, const void* W, int64_t 
   if (rope_mode != VGGT_ROPE_NONE && (!pos || !cos_tab || !sin_tab || period <= 0 || tab_len <= 0))
     return VGGT_ERR_SHAPE;
   if ((lda % 8) || (ldw % 8) || (ldo % 8) || ((uintptr_t)A & 15) || ((uintptr_t)W & 15) || ((uintptr_t)bias & 15) ||
-      ((uintptr_t)out & 15))
+      ((uintptr_t)out & 15) || (rope_mode != VGGT_ROPE_NONE && (((uintptr_t)cos_tab | (uintptr_t)sin_tab) & 15)))
     return VGGT_ERR_ALIGN;
   Epi ep{bias, out, ldo, nullptr, nullptr, 0, qw, qb, kw, kb, eps, hd, rope_mode, period, tab_len, pos, cos_tab,
          sin_tab};

@@ -181,12 +181,18 @@ __global__ __launch_bounds__(256) void headnorm_rope_kernel(const bf16_t* src, i
       const int er = e0 % RD;      // element index inside the rotated block
       const int pp = (MODE == VGGT_ROPE_2D && e0 >= D / 2) ? p1 : p0;
       const bool first = er < RD / 2;
+      // 8 consecutive table entries from a 32-B aligned offset: two 16-B loads each
+      const float4* cp = (const float4*)(cs + pp * RD + er);
+      const float4* sp = (const float4*)(sn + pp * RD + er);
+      const float4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
+      const float cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
       float y[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float partner = __shfl_xor(x[j], PL, 64);
         const float rot = first ? -partner : partner;
-        y[j] = x[j] * cs[pp * RD + er + j] + rot * sn[pp * RD + er + j];
+        y[j] = x[j] * cv[j] + rot * sv[j];
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) x[j] = y[j];
@@ -269,6 +275,7 @@ extern "C" int vggt_headnorm_rope(void* buf, int64_t ld, int col_off, int M, int
   if ((ld % 8) || (col_off % 8) || ((uintptr_t)buf % 16)) return VGGT_ERR_ALIGN;
   if (rope_mode != VGGT_ROPE_NONE && (!pos || !cos_tab || !sin_tab || period <= 0 || tab_len <= 0))
     return VGGT_ERR_SHAPE;
+  if (((uintptr_t)cos_tab | (uintptr_t)sin_tab) % 16) return VGGT_ERR_ALIGN;
   hipStream_t s = (hipStream_t)stream;
   if (D == 64) return launch_hnr<64>((const bf16_t*)buf, ld, (bf16_t*)buf, ld, col_off, M, H, w, b, eps, rope_mode, pos, period, cos_tab, sin_tab,
                                      tab_len, s, H, w, b);
@@ -285,6 +292,7 @@ extern "C" int vggt_qknorm_rope(void* qkv, int64_t ld, int M, int H, int D, cons
   if ((qw == nullptr) != (kw == nullptr)) return VGGT_ERR_SHAPE;
   if (rope_mode != VGGT_ROPE_NONE && (!pos || !cos_tab || !sin_tab || period <= 0 || tab_len <= 0))
     return VGGT_ERR_SHAPE;
+  if (((uintptr_t)cos_tab | (uintptr_t)sin_tab) % 16) return VGGT_ERR_ALIGN;
   hipStream_t s = (hipStream_t)stream;
   if (D == 64) return launch_hnr<64>((const bf16_t*)qkv, ld, (bf16_t*)qkv, ld, 0, M, 2 * H, qw, qb, eps, rope_mode, pos, period, cos_tab,
                                      sin_tab, tab_len, s, H, kw, kb);
@@ -306,6 +314,7 @@ extern "C" int vggt_qknorm_rope_out(const void* src, int64_t lds, void* dst, int
   if ((qw == nullptr) != (kw == nullptr)) return VGGT_ERR_SHAPE;
   if (rope_mode != VGGT_ROPE_NONE && (!pos || !cos_tab || !sin_tab || period <= 0 || tab_len <= 0))
     return VGGT_ERR_SHAPE;
+  if (((uintptr_t)cos_tab | (uintptr_t)sin_tab) % 16) return VGGT_ERR_ALIGN;
   hipStream_t s = (hipStream_t)stream;
   if (D == 64) return launch_hnr<64>((const bf16_t*)src, lds, (bf16_t*)dst, ldd, 0, M, 2 * H, qw, qb, eps, rope_mode,
                                      pos, period, cos_tab, sin_tab, tab_len, s, H, kw, kb);
@@ -324,6 +333,7 @@ extern "C" int vggt_headnorm_rope_out(const void* src, int64_t lds, void* dst, i
   if ((lds % 8) || (ldd % 8) || ((uintptr_t)src % 16) || ((uintptr_t)dst % 16)) return VGGT_ERR_ALIGN;
   if (rope_mode != VGGT_ROPE_NONE && (!pos || !cos_tab || !sin_tab || period <= 0 || tab_len <= 0))
     return VGGT_ERR_SHAPE;
+  if (((uintptr_t)cos_tab | (uintptr_t)sin_tab) % 16) return VGGT_ERR_ALIGN;
   hipStream_t s = (hipStream_t)stream;
   if (D == 64) return launch_hnr<64>((const bf16_t*)src, lds, (bf16_t*)dst, ldd, 0, M, H, w, b, eps, rope_mode, pos,
                                      period, cos_tab, sin_tab, tab_len, s, H, w, b);
