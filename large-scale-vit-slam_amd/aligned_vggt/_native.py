@@ -125,6 +125,7 @@ def version() -> str:
 TUNE_GEMM_TILE = 1
 TUNE_ATTN_WAVES = 2
 TUNE_ATTN_VARIANT = 3
+TUNE_CONV_PF2 = 4
 
 
 def tune(knob: int, value: int) -> int:

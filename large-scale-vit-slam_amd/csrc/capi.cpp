@@ -17,6 +17,7 @@ int env_or(const char* name, int dflt) {
 int g_vggt_gemm_tile = env_or("VGGT_GEMM", -1);
 int g_vggt_attn_waves = env_or("VGGT_ATTN_WAVES", 4);
 int g_vggt_attn_variant = env_or("VGGT_ATTN_VARIANT", 33);
+int g_vggt_conv_pf2 = env_or("VGGT_CONV_PF2", 1);
 
 extern "C" int vggt_tune(int knob, int value) {
   int prev;
@@ -40,6 +41,11 @@ extern "C" int vggt_tune(int knob, int value) {
         return VGGT_ERR_UNSUPPORTED;
       prev = g_vggt_attn_variant;
       g_vggt_attn_variant = value;
+      return prev;
+    case VGGT_TUNE_CONV_PF2:
+      if (value != 0 && value != 1) return VGGT_ERR_UNSUPPORTED;
+      prev = g_vggt_conv_pf2;
+      g_vggt_conv_pf2 = value;
       return prev;
     default: return VGGT_ERR_UNSUPPORTED;
   }

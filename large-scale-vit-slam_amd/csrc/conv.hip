@@ -17,6 +17,7 @@
 #include <math.h>
 
 #include "common.h"
+#include "tune.h"
 
 namespace {
 
@@ -221,9 +222,9 @@ __device__ __forceinline__ void cdma16(int32x4c rsrc, uint32_t voff, uint32_t so
                : "memory");
 }
 
-template <int BNX>
+template <int BNX, bool PF2>
 __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf16_t* __restrict__ whi,
-                                                            const bf16_t* __restrict__ wlo) {
+                                                            const bf16_t* __restrict__ wlo, uint32_t xbytes) {
   constexpr int NTN = BNX / 32;                       // 16-col fragments per wave (2 waves along N)
   constexpr int AT = BM * BK * 2, WT = BNX * BK * 2;  // bytes of one bf16 A / W tile
   constexpr int STG = 2 * AT + 2 * WT;               // Ahi, Alo, Whi, Wlo
@@ -319,6 +320,24 @@ __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf
         ra[i] = *(const f32x4*)(a.x + (((int64_t)pn[i] * a.hi + iy) * a.wi + ix) * a.ldx + ci0);
     }
   };
+  // PF2: the gather as raw buffer loads -- every lane issues exactly its 4
+  // loads (taps outside the image get an offset past num_records and read
+  // zeros), so the K-loop can wait with a COUNTED vmcnt and keep the next
+  // step's gather in flight across a barrier (two register stages)
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, (int)xbytes, 0x00020000);
+  auto load2 = [&](Stage& st, int kt) {
+    const int tap = kt % ntap;
+    const int ci0 = (kt / ntap) * BK + c4 * 4;
+    const int ky = tap / a.kw, kx = tap % a.kw;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int iy = py[i] + ky, ix = px[i] + kx;
+      const bool ok = pv[i] && iy >= 0 && iy < a.hi && ix >= 0 && ix < a.wi;
+      const uint32_t off = ok ? (uint32_t)((((pn[i] * a.hi + iy) * a.wi + ix) * (uint32_t)a.ldx + ci0) * 4u)
+                              : 0xfffffff0u;
+      st.ra[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)off, 0, 0));
+    }
+  };
   auto store = [&](const Stage& st, int buf) {
     char* base = smem + buf * STG;
 #pragma unroll
@@ -379,6 +398,59 @@ __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf
   // buffer, the A gather of tile kt+1 into registers, the MFMAs of tile kt,
   // the split + store of A tile kt+1, then every wave's DMA retired
   // (vmcnt(0)) before the barrier that publishes the next buffer.
+  if constexpr (PF2) {
+    // Two register stages, loop unrolled by two (s0 <-> buffer 0, s1 <->
+    // buffer 1, no loop-carried copies): in step kt the gather of tile kt+2
+    // is issued before the MFMAs of tile kt and stays in flight across the
+    // step's barrier (vmcnt(4) = only this step's 4 gather loads may remain;
+    // the W DMA and the previous gather are older).
+    Stage s1;
+    wstage(0, 0);
+    load2(s0, 0);
+    store(s0, 0);
+    if (nk > 1) {
+      load2(s1, 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    // steady state: every operation unconditional, so the compiler's own
+    // waitcnt tracking sees the same pending loads on both loop entries
+    int kt = 0;
+    for (; kt + 3 < nk; kt += 2) {
+      wstage(1, kt + 1);
+      load2(s0, kt + 2);
+      compute(0);
+      store(s1, 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      __syncthreads();
+      wstage(0, kt + 2);
+      load2(s1, kt + 3);
+      compute(1);
+      store(s0, 0);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      __syncthreads();
+    }
+    // the last 1-3 steps (no gather beyond tile kt+2)
+    const bool h1 = kt + 1 < nk, h2 = kt + 2 < nk;
+    if (h1) wstage(1, kt + 1);
+    if (h2) load2(s0, kt + 2);
+    compute(0);
+    if (h1) {
+      store(s1, 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (h2) wstage(0, kt + 2);
+      compute(1);
+      if (h2) {
+        store(s0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        compute(0);
+      }
+    }
+  } else {
   wstage(0, 0);
   load(s0, 0);
   store(s0, 0);
@@ -394,6 +466,7 @@ __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf
     if (kt + 1 < nk) store(s0, cur ^ 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  }
   }
 
   conv_epilogue<NTN>(a, acc, M, m0, n0, wm, wn, r16, q);
@@ -528,14 +601,24 @@ extern "C" int vggt_conv2d_bf16x3(const float* x, int64_t ldx, int nimg, int hi,
   if (((uintptr_t)w_hi % 16) || ((uintptr_t)w_lo % 16)) return VGGT_ERR_ALIGN;
   // 128-wide N tiles when there are at least 128 GEMM columns (more MFMA work
   // per split of the activation tile), else 64
+  // two-deep gather (buffer loads with 32-bit byte offsets) when the input spans < 4 GiB
+  const int64_t xb = ((int64_t)nimg * hi * wi - 1) * ldx * 4 + (int64_t)ci * 4;
+  const bool pf2 = xb < (int64_t)0xffffff00ll && g_vggt_conv_pf2;
+  const uint32_t xbytes = pf2 ? (uint32_t)xb : 0u;
+  hipStream_t s = (hipStream_t)stream;
+  const bf16_t *wh = (const bf16_t*)w_hi, *wl = (const bf16_t*)w_lo;
+#define VGGT_CONV(BNX, G)                                                            \
+  (pf2 ? conv_bf16x3_kernel<BNX, true><<<(int)(G), NT, 0, s>>>(a, wh, wl, xbytes)   \
+       : conv_bf16x3_kernel<BNX, false><<<(int)(G), NT, 0, s>>>(a, wh, wl, xbytes))
   if (a.ncols >= 128) {
     const int64_t nw2 = (nwg / ((a.ncols + BN - 1) / BN)) * ((a.ncols + 127) / 128);
-    conv_bf16x3_kernel<128><<<(int)nw2, NT, 0, (hipStream_t)stream>>>(a, (const bf16_t*)w_hi, (const bf16_t*)w_lo);
+    VGGT_CONV(128, nw2);
   } else if (a.ncols > 32) {
-    conv_bf16x3_kernel<64><<<(int)nwg, NT, 0, (hipStream_t)stream>>>(a, (const bf16_t*)w_hi, (const bf16_t*)w_lo);
+    VGGT_CONV(64, nwg);
   } else {  // output_conv2 (128 -> 32): 32-wide N tiles, no padded MFMA columns
-    conv_bf16x3_kernel<32><<<(int)nwg, NT, 0, (hipStream_t)stream>>>(a, (const bf16_t*)w_hi, (const bf16_t*)w_lo);
+    VGGT_CONV(32, nwg);
   }
+#undef VGGT_CONV
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
 }

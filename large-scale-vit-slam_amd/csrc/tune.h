@@ -3,3 +3,4 @@
 extern int g_vggt_gemm_tile;   // -1 auto, 0 128x128, 1 256x256 ring, 2 256x128 ring
 extern int g_vggt_attn_waves;  // 4 or 8
 extern int g_vggt_attn_variant; // attention schedule variant bits (attention.hip)
+extern int g_vggt_conv_pf2;     // split-bf16 conv: 1 two-deep buffer-load gather, 0 one-deep

@@ -16,6 +16,13 @@ for (n, hw, ci, co) in [(16, 148, 256, 256), (16, 296, 256, 128), (16, 74, 256, 
     whi, wlo = N.split_bf16x2(wp)
     b = torch.zeros(co, device=dev)
     y = torch.empty(n * hw * hw, co, device=dev)
-    us = timeit(lambda: N.conv2d_bf16x3(x, n, hw, hw, ci, whi, wlo, b, co, 3, 3, 1, 1, y))
     fl = 2 * n * hw * hw * co * 9 * ci
-    print(f"conv3x3 n={n} hw={hw} ci={ci} co={co}: {us:.1f} us  alg {fl/us/1e6:.0f} TF/s  mfma {3*fl/us/1e6:.0f} TF/s", flush=True)
+    outs = {}
+    for pf2 in (0, 1, 0, 1):  # A/B of the gather depth (VGGT_TUNE_CONV_PF2), same process
+        N.tune(N.TUNE_CONV_PF2, pf2)
+        us = timeit(lambda: N.conv2d_bf16x3(x, n, hw, hw, ci, whi, wlo, b, co, 3, 3, 1, 1, y))
+        outs[pf2] = y.clone()
+        print(f"conv3x3 n={n} hw={hw} ci={ci} co={co} pf2={pf2}: {us:.1f} us  alg {fl/us/1e6:.0f} TF/s  "
+              f"mfma {3*fl/us/1e6:.0f} TF/s", flush=True)
+    print("  pf2 == one-deep bitwise:", torch.equal(outs[0], outs[1]), flush=True)
+    N.tune(N.TUNE_CONV_PF2, 1)

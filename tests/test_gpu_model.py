@@ -197,11 +197,22 @@ def test_sequence_ate_rpe_parity(models):
         return {**ate.compute(), **rpe.compute()}
 
     assert got["pose_enc"].shape == (1, S, 9)
-    m_hip, m_ref, m_32 = metrics(got["pose_enc"]), metrics(oracle_seq(True)), metrics(oracle_seq(False))
+    pe_ref, pe_32 = oracle_seq(True), oracle_seq(False)
+    pe_hip = got["pose_enc"].cpu()
+    # the merged, GT-scale-aligned trajectory itself: translation / quaternion / FoV parts
+    for sl, name in ((slice(0, 3), "t"), (slice(3, 7), "q"), (slice(7, 9), "fov")):
+        e_hip, e_32 = _rel(pe_hip[..., sl], pe_ref[..., sl]), _rel(pe_32[..., sl], pe_ref[..., sl])
+        print(f"pose_enc[{name}] rel vs bf16 oracle: hip {e_hip:.3e}  fp32 oracle {e_32:.3e}")
+        assert e_hip < max(2e-2, 3 * e_32), (name, e_hip, e_32)
+    m_hip, m_ref, m_32 = metrics(pe_hip), metrics(pe_ref), metrics(pe_32)
     print("hip", m_hip, "\nref bf16", m_ref, "\nref fp32", m_32)
+    # ATE / RPE of a random-weight trajectory (RPE-rot ~90 deg) amplify the
+    # pose differences above: the oracle's own metrics move by several % between
+    # boxes (CPU thread count -> fp32 summation order), so the metric bar is 10%
+    # (the metric code itself is pinned by golden fixtures, test_eval_alignment.py)
     for k in m_ref:
         spread = abs(m_32[k] - m_ref[k])
-        assert abs(m_hip[k] - m_ref[k]) <= max(5e-2 * abs(m_ref[k]), 1.5 * spread) + 1e-6, (k, m_hip, m_ref, m_32)
+        assert abs(m_hip[k] - m_ref[k]) <= max(1e-1 * abs(m_ref[k]), 1.5 * spread) + 1e-6, (k, m_hip, m_ref, m_32)
 
 
 def test_feature_aligned_batch2(models):
