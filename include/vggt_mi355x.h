@@ -105,6 +105,21 @@ int vggt_layernorm(const void* x, int in_dtype, int64_t ldx, const float* w, con
                    void* y, int out_dtype, int64_t ldy, void* stream);
 
 /*
+ * Residual LayerScale add fused with the NEXT LayerNorm:
+ *   x[m] += gamma * y[m]          (x fp32 [M, C] in place, y bf16 [M, C])
+ *   out2[m] = x[m]                (if out2 != NULL: the kept-layer concat half)
+ *   xn[m] = LayerNorm(x[m]; w, b) (bf16, if xn != NULL; w/b may be NULL)
+ * The add is the arithmetic of vggt_gemm_bf16's VGGT_EPI_RESID_F32 epilogue
+ * on the bf16-rounded branch output.  Replaces `x = x + ls2(mlp(norm2(x)))`
+ * followed by the next block's `norm1(x)` (vggt layers/block.py, ext; the
+ * aggregator's frame/global alternation, featureAligned_vggt.py:78-82).
+ * C a multiple of 256 in {256, 512, 1024, 2048}.
+ */
+int vggt_resid_add_layernorm(float* x, int64_t ldx, const void* y, int64_t ldy, const float* gamma, float* out2,
+                             int64_t ldo2, const float* w, const float* b, float eps, int M, int C, void* xn,
+                             int64_t ldn, void* stream);
+
+/*
  * In-place per-head LayerNorm (QK-norm) + RoPE on a bf16 [M, ld] buffer:
  * for each row m and head h, the D values at columns col_off + h*D are
  * normalised with (w,b,eps) (skipped if w == NULL) and rotated (rope_mode).

@@ -31,6 +31,7 @@ _SIGS = {
     "vggt_gemm_qkv": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _vp, _i64, _vp, _vp, _vp, _vp, _f, _i, _vp, _i, _vp,
                       _vp, _i, _vp],
     "vggt_layernorm": [_vp, _i, _i64, _vp, _vp, _f, _i, _i, _vp, _i, _i64, _vp],
+    "vggt_resid_add_layernorm": [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _f, _i, _i, _vp, _i64, _vp],
     "vggt_headnorm_rope": [_vp, _i64, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _i, _vp, _vp, _i, _vp],
     "vggt_attention_fwd": [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i, _i, _i, _i, _i, _f,
                            _vp],
@@ -215,6 +216,22 @@ def layernorm(x: torch.Tensor, w: Optional[torch.Tensor], b: Optional[torch.Tens
                               _ld(out), _stream())
     _check(rc, "vggt_layernorm")
     return out
+
+
+def resid_add_layernorm(x: torch.Tensor, y: torch.Tensor, gamma: torch.Tensor, out2: Optional[torch.Tensor],
+                        w: Optional[torch.Tensor], b: Optional[torch.Tensor], eps: float,
+                        xn: Optional[torch.Tensor]) -> None:
+    """x += gamma * y (fp32 residual, bf16 branch output; the GEMM EPI_RESID_F32
+    arithmetic), mirrored into out2 if given, then xn = LayerNorm(x) in bf16 if
+    xn is given (one HBM pass instead of the epilogue RMW + a LayerNorm)."""
+    _dev(x, "resid_add_layernorm")
+    M, C = x.shape
+    assert x.dtype == torch.float32 and y.dtype == torch.bfloat16 and y.shape[0] == M and y.shape[1] == C
+    assert xn is None or (xn.dtype == torch.bfloat16 and xn.shape[0] == M and xn.shape[1] == C)
+    rc = lib().vggt_resid_add_layernorm(_p(x), _ld(x), _p(y), _ld(y), _p(gamma), _p(out2),
+                                        _ld(out2) if out2 is not None else 0, _p(w), _p(b), float(eps), M, C, _p(xn),
+                                        _ld(xn) if xn is not None else 0, _stream())
+    _check(rc, "vggt_resid_add_layernorm")
 
 
 def headnorm_rope(buf: torch.Tensor, col_off: int, H: int, D: int, w: Optional[torch.Tensor],

@@ -183,8 +183,10 @@ class Aggregator(nn.Module):
         N.dino_assemble(pe, dino.cls_token.detach().float().contiguous(),
                         dino.register_tokens.detach().float().contiguous(), dino.pos_embed_for(h, w), F_, hw, nreg, C,
                         x)
-        for blk in dino.blocks:
-            blk.forward_rows(x, M, (F_, P, P), None, ws, tag="dino_attn")
+        ready = False
+        for j, blk in enumerate(dino.blocks):
+            nxt = dino.blocks[j + 1].norm1 if j + 1 < len(dino.blocks) else None
+            ready = blk.forward_rows(x, M, (F_, P, P), None, ws, tag="dino_attn", xn_ready=ready, next_norm=nxt)
 
         # ---- aggregator tokens: final DINOv2 norm + camera/register tokens
         y = ws.buf("agg_x", round_up(M, 256), C)
@@ -193,10 +195,15 @@ class Aggregator(nn.Module):
         rope = self._rope_tables(h, w, images.device) if self.rope is not None else None
 
         outs = {i: torch.empty(B, S, P, 2 * C, device=images.device, dtype=torch.float32) for i in keep}
+        # each block's last residual add also writes the next block's norm1(y)
+        ready = False
         for i in range(self.depth):
             o = outs[i].view(M, 2 * C) if i in outs else None
-            self.frame_blocks[i].forward_rows(y, M, (F_, P, P), rope, ws, out2=o[:, :C] if o is not None else None,
-                                              tag="frame_attn")
-            self.global_blocks[i].forward_rows(y, M, (B, S * P, S * P), rope, ws,
-                                               out2=o[:, C:] if o is not None else None, tag="global_attn")
+            ready = self.frame_blocks[i].forward_rows(y, M, (F_, P, P), rope, ws,
+                                                      out2=o[:, :C] if o is not None else None, tag="frame_attn",
+                                                      xn_ready=ready, next_norm=self.global_blocks[i].norm1)
+            nxt = self.frame_blocks[i + 1].norm1 if i + 1 < self.depth else None
+            ready = self.global_blocks[i].forward_rows(y, M, (B, S * P, S * P), rope, ws,
+                                                       out2=o[:, C:] if o is not None else None, tag="global_attn",
+                                                       xn_ready=ready, next_norm=nxt)
         return [outs[i] for i in keep], self.patch_start_idx

@@ -70,6 +70,12 @@ class Attention(nn.Module):
 # q/k norm + RoPE fused into the qkv GEMM epilogue (vggt_gemm_qkv); VGGT_FUSED_QKV=0
 # selects the separate headnorm_rope launch (A/B and fallback for odd shapes).
 _FUSED_QKV = os.environ.get("VGGT_FUSED_QKV", "1") != "0"
+# VGGT_FUSED_ADD_LN=1: fc2 as a plain GEMM + one fused residual-add /
+# next-LayerNorm row pass (vggt_resid_add_layernorm).  Off by default: in the
+# model (r2c, same box) plain fc2 226.6 us + the row pass 44.8 us - the saved
+# norm1 24.6 us = 246.8 us vs 235.2 us for the fp32 read-modify-write epilogue
+# of the 128x128 form (whose two workgroups per CU overlap the RMW).
+_FUSED_ADD_LN = os.environ.get("VGGT_FUSED_ADD_LN", "0") == "1"
 
 
 class RopeTables:
@@ -120,18 +126,26 @@ class Block(nn.Module):
 
     @torch.no_grad()
     def forward_rows(self, x: torch.Tensor, M: int, groups: Tuple[int, int, int], rope: Optional[RopeTables],
-                     ws: Workspace, out2: Optional[torch.Tensor] = None, tag: Optional[str] = None) -> None:
+                     ws: Workspace, out2: Optional[torch.Tensor] = None, tag: Optional[str] = None,
+                     xn_ready: bool = False, next_norm: Optional[nn.LayerNorm] = None) -> bool:
         """In-place ``x[:M] = Block(x[:M])`` on the row-major fp32 residual
         stream x [>=M, C].  Attention is grouped as ``groups = (batch,
         rows_per_group, n)``: frame attention (B*S, P, P), global attention
         (B, S*P, S*P).  Optionally mirrors the block output into ``out2``
-        (an fp32 [M, C] strided view, e.g. one half of a concat buffer)."""
+        (an fp32 [M, C] strided view, e.g. one half of a concat buffer).
+
+        ``xn_ready``: the workspace's ``blk_xn`` already holds norm1(x) (the
+        previous block fused it into its last residual add).  ``next_norm``:
+        the LayerNorm the caller applies to x next (the following block's
+        norm1); the fc2 residual add then also writes next_norm(x) into
+        ``blk_xn`` in the same pass.  Returns True when it did."""
         C = x.shape[1]
         H = self.attn.num_heads
         D = C // H
         xs = x[:M]
         xn = ws.buf("blk_xn", M, C, torch.bfloat16)
-        N.layernorm(xs, self.norm1.weight, self.norm1.bias, self.norm1.eps, xn)
+        if not xn_ready:
+            N.layernorm(xs, self.norm1.weight, self.norm1.bias, self.norm1.eps, xn)
         w, b = pack_linear(self.attn.qkv)
         qkv = ws.buf("blk_qkv", M, 3 * C, torch.bfloat16)
         qn = self.attn.q_norm if isinstance(self.attn.q_norm, nn.LayerNorm) else None
@@ -164,7 +178,18 @@ class Block(nn.Module):
         hid = ws.buf("blk_h", M, w.shape[0], torch.bfloat16)
         N.gemm_bf16(xn, w, b, hid, N.EPI_GELU_BF16)
         w, b = pack_linear(self.mlp.fc2)
-        N.gemm_bf16(hid, w, b, xs, N.EPI_RESID_F32, gamma=self._gamma(self.ls2, C, x.device), out2=out2)
+        if not (_FUSED_ADD_LN and C % 256 == 0 and C <= 2048):
+            N.gemm_bf16(hid, w, b, xs, N.EPI_RESID_F32, gamma=self._gamma(self.ls2, C, x.device), out2=out2)
+            return False
+        # fc2 with a plain bf16 epilogue, then ONE row pass for the LayerScale
+        # residual add, the kept-layer mirror and the next block's norm1 (same
+        # arithmetic as the EPI_RESID_F32 epilogue).
+        N.gemm_bf16(hid, w, b, ao, N.EPI_BF16)
+        ln = next_norm if isinstance(next_norm, nn.LayerNorm) else None
+        N.resid_add_layernorm(xs, ao, self._gamma(self.ls2, C, x.device), out2,
+                              ln.weight if ln is not None else None, ln.bias if ln is not None else None,
+                              ln.eps if ln is not None else 0.0, xn if ln is not None else None)
+        return ln is not None
 
     @torch.no_grad()
     def forward_f32(self, x: torch.Tensor) -> torch.Tensor:

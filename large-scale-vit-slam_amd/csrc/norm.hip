@@ -92,6 +92,84 @@ int launch_ln(const void* x, int in_bf, int64_t ldx, const float* w, const float
   return VGGT_OK;
 }
 
+// ------------------------------------ LayerScale residual add + LayerNorm
+// x[m] += gamma * y[m] (fp32 residual, bf16 branch output -- the arithmetic
+// of the GEMM's EPI_RESID_F32 epilogue), optionally mirrored into out2, then
+// (LN) xn[m] = LayerNorm(x[m]) in bf16, affine when w is given.  One wave per
+// row, NV float4 per lane, like layernorm_kernel.
+template <int NV, bool LN>
+__global__ __launch_bounds__(256) void resid_add_ln_kernel(float* __restrict__ x, int64_t ldx,
+                                                           const bf16_t* __restrict__ y, int64_t ldy,
+                                                           const float* __restrict__ gamma, float* __restrict__ out2,
+                                                           int64_t ldo2, const float* __restrict__ w,
+                                                           const float* __restrict__ b, float eps, int M,
+                                                           bf16_t* __restrict__ xn, int64_t ldn) {
+  constexpr int C = NV * 256;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float v[NV][4];
+  uint2 yu[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) yu[i] = *(const uint2*)(y + (int64_t)row * ldy + i * 256 + lane * 4);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = i * 256 + lane * 4;
+    const f32x4 u = *(const f32x4*)(x + (int64_t)row * ldx + c);
+    const f32x4 g = *(const f32x4*)(gamma + c);
+    const float yv[4] = {bf2f(yu[i].x & 0xffff), bf2f(yu[i].x >> 16), bf2f(yu[i].y & 0xffff), bf2f(yu[i].y >> 16)};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[i][j] = u[j] + g[j] * yv[j];
+    *(f32x4*)(x + (int64_t)row * ldx + c) = f32x4{v[i][0], v[i][1], v[i][2], v[i][3]};
+    if (out2) *(f32x4*)(out2 + (int64_t)row * ldo2 + c) = f32x4{v[i][0], v[i][1], v[i][2], v[i][3]};
+  }
+  if constexpr (LN) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s += v[i][j];
+    const float mean = wave_sum(s) * (1.f / C);
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = v[i][j] - mean;
+        q += d * d;
+      }
+    const float rstd = rsqrtf(wave_sum(q) * (1.f / C) + eps);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = i * 256 + lane * 4;
+      float o[4];
+      if (w) {
+        const f32x4 wv = *(const f32x4*)(w + c);
+        const f32x4 bv = b ? *(const f32x4*)(b + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd * wv[j] + bv[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd;
+      }
+      uint2 u;
+      u.x = pack_bf2(o[0], o[1]);
+      u.y = pack_bf2(o[2], o[3]);
+      *(uint2*)(xn + (int64_t)row * ldn + c) = u;
+    }
+  }
+}
+
+template <int NV>
+void launch_raln(float* x, int64_t ldx, const bf16_t* y, int64_t ldy, const float* gamma, float* out2, int64_t ldo2,
+                 const float* w, const float* b, float eps, int M, bf16_t* xn, int64_t ldn, hipStream_t s) {
+  const int grid = (M + 3) / 4;
+  if (xn)
+    resid_add_ln_kernel<NV, true><<<grid, 256, 0, s>>>(x, ldx, y, ldy, gamma, out2, ldo2, w, b, eps, M, xn, ldn);
+  else
+    resid_add_ln_kernel<NV, false><<<grid, 256, 0, s>>>(x, ldx, y, ldy, gamma, out2, ldo2, w, b, eps, M, xn, ldn);
+}
+
 // ------------------------------------------------- per-head norm + RoPE
 // One wave per row; each lane owns 8 consecutive values (one 16-B chunk) of
 // a head; LPH = D/8 lanes per head, heads processed 64/LPH at a time.
@@ -265,6 +343,29 @@ extern "C" int vggt_layernorm(const void* x, int in_dtype, int64_t ldx, const fl
                               int M, int C, void* y, int out_dtype, int64_t ldy, void* stream) {
   return vggt_layernorm_grouped(x, in_dtype, ldx, w, b, eps, M, C, y, out_dtype, ldy, M > 0 ? M : 1, 0, 0, 0, 0,
                                 stream);
+}
+
+extern "C" int vggt_resid_add_layernorm(float* x, int64_t ldx, const void* y, int64_t ldy, const float* gamma,
+                                        float* out2, int64_t ldo2, const float* w, const float* b, float eps, int M,
+                                        int C, void* xn, int64_t ldn, void* stream) {
+  if (M <= 0) return M == 0 ? VGGT_OK : VGGT_ERR_SHAPE;
+  if (C % 256 || C > 4096 || C <= 0 || !x || !y || !gamma) return VGGT_ERR_SHAPE;
+  if ((ldx % 4) || (ldy % 4) || (out2 && (ldo2 % 4)) || (xn && (ldn % 4))) return VGGT_ERR_ALIGN;
+  if (((uintptr_t)x | (uintptr_t)gamma | (uintptr_t)out2) % 16 || ((uintptr_t)y | (uintptr_t)xn) % 8)
+    return VGGT_ERR_ALIGN;
+  if ((w && ((uintptr_t)w % 16)) || (b && ((uintptr_t)b % 16))) return VGGT_ERR_ALIGN;
+  hipStream_t s = (hipStream_t)stream;
+  const bf16_t* yb = (const bf16_t*)y;
+  bf16_t* nb = (bf16_t*)xn;
+  switch (C / 256) {
+    case 1: launch_raln<1>(x, ldx, yb, ldy, gamma, out2, ldo2, w, b, eps, M, nb, ldn, s); break;
+    case 2: launch_raln<2>(x, ldx, yb, ldy, gamma, out2, ldo2, w, b, eps, M, nb, ldn, s); break;
+    case 4: launch_raln<4>(x, ldx, yb, ldy, gamma, out2, ldo2, w, b, eps, M, nb, ldn, s); break;
+    case 8: launch_raln<8>(x, ldx, yb, ldy, gamma, out2, ldo2, w, b, eps, M, nb, ldn, s); break;
+    default: return VGGT_ERR_SHAPE;
+  }
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
 }
 
 extern "C" int vggt_headnorm_rope(void* buf, int64_t ld, int col_off, int M, int H, int D, const float* w,

@@ -55,3 +55,24 @@ def test_aggregator_full_depth_two_frames(cuda):
 def test_aggregator_batch2(cuda):
     outs, ref, _ = _run(cuda, depth=2, dino_depth=1, B=2, S=2, H=42, W=56, keep=(1,))
     assert _rel(outs[0], ref[0]) < 2e-2
+
+
+def test_aggregator_fused_add_ln_matches_epilogue_path(cuda, monkeypatch):
+    """fc2 as plain GEMM + fused residual-add / next-norm1 pass (default) vs the
+    fp32 read-modify-write epilogue + separate LayerNorm: same arithmetic, so
+    the kept-layer outputs agree to fp32 accumulation-order noise."""
+    from aligned_vggt.backbone import layers as L
+    from aligned_vggt.backbone.aggregator import Aggregator
+    from aligned_vggt.utils.synthetic import synthetic_init_, synthetic_images
+    agg = Aggregator(depth=4, dino_depth=3)
+    synthetic_init_(agg, seed=5)
+    agg = agg.to(cuda)
+    img = synthetic_images(1, 3, 112, 126).to(cuda)
+    monkeypatch.setattr(L, "_FUSED_ADD_LN", True)
+    a, _ = agg(img, keep_layers=(0, 3))
+    a = [t.clone() for t in a]
+    monkeypatch.setattr(L, "_FUSED_ADD_LN", False)
+    b, _ = agg(img, keep_layers=(0, 3))
+    torch.cuda.synchronize()
+    for u, v in zip(a, b):
+        assert _rel(u, v) < 2e-3, _rel(u, v)

@@ -115,6 +115,41 @@ def test_layernorm(N, C, ib, ob):
     assert _rel(out, ref) < (4e-3 if ob else 1e-5)
 
 
+@pytest.mark.parametrize("C", [256, 1024, 2048])
+@pytest.mark.parametrize("ln,mirror,affine", [(True, True, True), (True, False, False), (False, True, True)])
+def test_resid_add_layernorm(N, C, ln, mirror, affine):
+    """x += gamma * y; out2 = x; xn = LayerNorm(x) (bf16) vs fp32 torch, on a
+    strided residual (ld > C) and a ragged row count."""
+    g = torch.Generator().manual_seed(C)
+    M = 301
+    xb = (torch.randn(M, C + 64, generator=g) * 3 + 1).cuda()
+    x = xb[:, :C]
+    pad = xb[:, C:].clone()
+    y = (torch.randn(M, C, generator=g)).to(torch.bfloat16).cuda()
+    gamma = (torch.rand(C, generator=g) * 0.5).cuda()
+    w = torch.randn(C, generator=g).cuda() if affine else None
+    b = torch.randn(C, generator=g).cuda() if affine else None
+    ref_x = x.clone() + gamma * y.float()
+    ref_n = F.layer_norm(ref_x, (C,), w, b, 1e-5)
+    o2 = torch.zeros(M, 2 * C, device="cuda")[:, C:] if mirror else None
+    xn = torch.empty(M, C, device="cuda", dtype=torch.bfloat16) if ln else None
+    N.resid_add_layernorm(x, y, gamma, o2, w, b, 1e-5, xn)
+    torch.cuda.synchronize()
+    assert _rel(x, ref_x) < 1e-6
+    assert torch.equal(xb[:, C:], pad)  # columns past C untouched
+    if mirror:
+        assert torch.equal(o2, x)
+    if ln:
+        assert _rel(xn, ref_n) < 4e-3
+
+
+def test_resid_add_layernorm_rejects(N):
+    x = torch.zeros(4, 768, device="cuda")
+    y = torch.zeros(4, 768, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="shape"):
+        N.resid_add_layernorm(x, y, torch.ones(768, device="cuda"), None, None, None, 1e-5, None)
+
+
 @pytest.mark.parametrize("D,mode", [(64, 1), (128, 1), (64, 0), (128, 2), (64, 2)])
 def test_headnorm_rope(N, D, mode):
     H = 1024 // D
@@ -360,9 +395,30 @@ def _online_softmax_rescale(N):
 def test_gemm_qkv_fused_matches_two_pass(N, tile, D, H, mode, norm):
     """vggt_gemm_qkv (q/k LayerNorm + RoPE in the GEMM epilogue) against the
     parity-tested two-launch path (gemm_bf16 + qknorm_rope)."""
+    _qkv_fused_check(N, tile, D, H, mode, norm, 1500, 256)
+
+
+@pytest.mark.parametrize("D,H,mode", [(64, 16, 1), (128, 8, 2)])
+def test_gemm_qkv_fused_production_rows(N, D, H, mode):
+    """Production row count (16 x 1374 tokens, auto tile: the 256x256 ping-pong
+    form with a ragged last row panel)."""
+    _qkv_fused_check(N, -1, D, H, mode, True, 21984, 1024)
+
+
+@pytest.mark.parametrize("Nn,epi", [(3072, 0), (4096, 1), (4096, 0), (3072, 2), (3072, 3)])
+def test_gemm_production_rows(N, Nn, epi):
+    """Every epilogue at M = 21984 on the 256x256 ping-pong form (86 x 12 or
+    86 x 16 tiles: a partial last round of workgroups, ragged last panel)."""
+    prev = N.tune(N.TUNE_GEMM_TILE, 4)
+    try:
+        test_gemm_epilogues(N, 21984, Nn, 1024, epi)
+    finally:
+        N.tune(N.TUNE_GEMM_TILE, prev)
+
+
+def _qkv_fused_check(N, tile, D, H, mode, norm, M, K):
     from aligned_vggt.backbone.layers import RopeTables
-    M, C = 1500, H * D
-    K = 256
+    C = H * D
     g = torch.Generator(device="cuda").manual_seed(D + H + mode)
     a = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
     w = (torch.randn(3 * C, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
