@@ -777,6 +777,22 @@ inline int pp_pick_bn(int M, int N, bool allow192) {
   return best;
 }
 
+// Auto width for the ping-pong form: 256-wide tiles where they fill at least
+// two rounds of CUs (measured best on the 21,984-row chunk shapes), else the
+// quantisation-aware pick.  Short M (the 154x518 sequence chunks, 6,592 rows)
+// would leave a partial last round almost empty: qkv N = 3072 at 256 wide is
+// 312 tiles = 1.22 rounds, at 192 wide 416 tiles = 1.63.
+inline int pp_auto_bn(int M, int N, bool allow192) {
+  static int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    return n;
+  }();
+  const long tiles256 = (long)((M + PBM - 1) / PBM) * (N / 256);
+  if (N % 256 == 0 && tiles256 >= 2l * cus) return 256;
+  return pp_pick_bn(M, N, allow192);
+}
+
 }  // namespace
 
 namespace {
@@ -807,14 +823,14 @@ int gemm_impl(const void* A, int64_t lda, const void* W, int64_t ldw, const floa
   // fc2 225 vs 234 us) and for small M.
   int mode = g_vggt_gemm_tile;
   if (mode < 0)
-    mode = (M >= 4096 && K % PBK == 0 && N % 256 == 0 && N >= 2048 && epi != VGGT_EPI_RESID_F32) ? 4 : 0;
+    mode = (M >= 4096 && K % PBK == 0 && N % 256 == 0 && N >= 2048 && epi != VGGT_EPI_RESID_F32) ? 7 : 0;
   if (mode >= 3 && K % PBK) mode = 2;    // the ping-pong form steps K by 64
   if (mode == 0 && K % BK) mode = 2;     // the 128x128 form steps K by 64
   if (mode == 1 && N % 256) mode = 2;
   // per-lane 32-bit DMA offsets span one 256-row panel
   if (mode != 0 && (int64_t)RBM * (lda > ldw ? lda : ldw) * 2 >= (1ll << 31)) return VGGT_ERR_SHAPE;
   if (mode >= 3) {
-    int bn = mode == 4 ? 256 : mode == 5 ? 192 : mode == 6 ? 128 : pp_pick_bn(M, N, true);
+    int bn = mode == 4 ? 256 : mode == 5 ? 192 : mode == 6 ? 128 : mode == 7 ? pp_auto_bn(M, N, true) : pp_pick_bn(M, N, true);
     if (bn == 0 || N % bn) bn = pp_pick_bn(M, N, true);
     if (bn == 0) return VGGT_ERR_SHAPE;
 #define VGGT_PP(E)                                                    \
@@ -900,14 +916,14 @@ extern "C" int vggt_gemm_qkv(const void* A, int64_t lda, const void* W, int64_t 
   // auto: the 256-wide ping-pong form on long M (fused qkv 179 vs 239 us for the
   // 128x128 form, r1s), the 128x128 form otherwise
   int mode = g_vggt_gemm_tile;
-  if (mode < 0) mode = (M >= 4096 && K % PBK == 0) ? (N % 256 == 0 ? 4 : 6) : 0;
+  if (mode < 0) mode = (M >= 4096 && K % PBK == 0) ? (N % 256 == 0 ? 7 : 6) : 0;
   if (mode >= 3 && K % PBK) mode = 2;
   if (mode == 0 && K % BK) mode = 2;
   if (mode == 1 && hd % 256) mode = 2;
   if (mode != 0 && (int64_t)RBM * (lda > ldw ? lda : ldw) * 2 >= (1ll << 31)) return VGGT_ERR_SHAPE;
   if (mode >= 3) {
     // 192-wide tiles only with 64-wide heads (the norm's lane groups stay aligned)
-    int bn = mode == 4 ? 256 : mode == 5 ? 192 : mode == 6 ? 128 : pp_pick_bn(M, N, D == 64);
+    int bn = mode == 4 ? 256 : mode == 5 ? 192 : mode == 6 ? 128 : mode == 7 ? pp_auto_bn(M, N, D == 64) : pp_pick_bn(M, N, D == 64);
     if (bn == 0 || N % bn || (bn == 192 && D != 64)) bn = pp_pick_bn(M, N, D == 64);
     if (bn == 0) return VGGT_ERR_SHAPE;
     if (D == 64) {

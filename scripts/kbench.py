@@ -42,11 +42,13 @@ def main():
     ap.add_argument("--attn-variants", default="0")
     ap.add_argument("--rounds", type=int, default=1, help="repeat the attention sweep (A/B alternation)")
     ap.add_argument("--warm-s", type=float, default=3.0)
+    ap.add_argument("--tokens", type=int, default=16 * 1374,
+                    help="token rows M (6592 = the 154x518 sequence chunk, 16 x 412)")
     args = ap.parse_args()
     only = set(args.only.split(","))
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
-    M, C, H, D = 16 * 1374, 1024, 16, 64
+    M, C, H, D = args.tokens, 1024, 16, 64
     res = {}
     if "gemm" in only:
         x = (torch.randn(M, 4096, device=dev) * 0.5).bfloat16()
