@@ -536,10 +536,13 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
   // 8-wave workgroups (256 query rows) for long sequences; 4-wave ones
   // (128 rows) when the query count is short enough that the padding of a
   // 256-row block would cost more than the pairing gains.
-  const int nw = (g_vggt_attn_waves == 8 && nq >= 4096) ? 8 : 4;
+  // 2-wave workgroups (64 query rows; only the default offset-free variant 33
+  // is instantiated) for grids that fill a fraction of one round of slots.
+  const bool two_ok = (g_vggt_attn_variant & 32) && (g_vggt_attn_variant & 65) == 1;
+  const int nw = (g_vggt_attn_waves == 8 && nq >= 4096) ? 8 : (g_vggt_attn_waves == 2 && two_ok) ? 2 : 4;
   const int nwg = ((nq + nw * 32 - 1) / (nw * 32)) * heads * batch;
   hipStream_t s = (hipStream_t)stream;
-  if ((g_vggt_attn_variant == 19 || g_vggt_attn_variant == 23) && D == 64) {  // pipelined QK^T (3 LDS slots)
+  if ((g_vggt_attn_variant == 19 || g_vggt_attn_variant == 23) && D == 64 && nw != 2) {  // pipelined QK^T (3 LDS slots)
     if (nw == 8) attn_fwd_kernel<64, 8, 19><<<nwg, 512, 0, s>>>(a);
     else if (g_vggt_attn_variant == 23) attn_fwd_kernel<64, 4, 23><<<nwg, 256, 0, s>>>(a);
     else attn_fwd_kernel<64, 4, 19><<<nwg, 256, 0, s>>>(a);
@@ -548,15 +551,16 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
   }
   if (g_vggt_attn_variant & 32) {  // offset-free softmax (bit 0 and the exact-score bit 64 combine)
     const int v = (g_vggt_attn_variant & 1) + ((g_vggt_attn_variant & 64) ? 2 : 0);
-    switch ((D == 64 ? 0 : 8) + (nw == 8 ? 4 : 0) + v) {
+    switch ((D == 64 ? 0 : 16) + (nw == 8 ? 4 : nw == 2 ? 8 : 0) + v) {
 #define VGGT_ATTN_SCASE(DD, NWW, V)                                                               \
-  case (DD == 64 ? 0 : 8) + (NWW == 8 ? 4 : 0) + V:                                                \
+  case (DD == 64 ? 0 : 16) + (NWW == 8 ? 4 : NWW == 2 ? 8 : 0) + V:                                \
     attn_fwd_kernel<DD, NWW, 32 + (V & 1) + ((V & 2) ? 64 : 0)><<<nwg, NWW * 64, 0, s>>>(a); \
     break;
       VGGT_ATTN_SCASE(64, 4, 0) VGGT_ATTN_SCASE(64, 4, 1) VGGT_ATTN_SCASE(64, 4, 2) VGGT_ATTN_SCASE(64, 4, 3)
       VGGT_ATTN_SCASE(64, 8, 0) VGGT_ATTN_SCASE(64, 8, 1) VGGT_ATTN_SCASE(64, 8, 2) VGGT_ATTN_SCASE(64, 8, 3)
       VGGT_ATTN_SCASE(128, 4, 0) VGGT_ATTN_SCASE(128, 4, 1) VGGT_ATTN_SCASE(128, 4, 2) VGGT_ATTN_SCASE(128, 4, 3)
       VGGT_ATTN_SCASE(128, 8, 0) VGGT_ATTN_SCASE(128, 8, 1) VGGT_ATTN_SCASE(128, 8, 2) VGGT_ATTN_SCASE(128, 8, 3)
+      VGGT_ATTN_SCASE(64, 2, 1) VGGT_ATTN_SCASE(128, 2, 1)
 #undef VGGT_ATTN_SCASE
       default: return VGGT_ERR_UNSUPPORTED;
     }

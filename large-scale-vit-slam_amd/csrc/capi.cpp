@@ -15,7 +15,7 @@ int env_or(const char* name, int dflt) {
 }  // namespace
 
 int g_vggt_gemm_tile = env_or("VGGT_GEMM", -1);
-int g_vggt_attn_waves = env_or("VGGT_ATTN_WAVES", 4);
+int g_vggt_attn_waves = env_or("VGGT_ATTN_WAVES", 8);  // 8-wave groups for nq >= 4096 (profiles/r2c/ab_attn_w8)
 int g_vggt_attn_variant = env_or("VGGT_ATTN_VARIANT", 33);
 int g_vggt_conv_pf2 = env_or("VGGT_CONV_PF2", 1);
 
@@ -30,7 +30,7 @@ extern "C" int vggt_tune(int knob, int value) {
       g_vggt_gemm_tile = value;
       return prev;
     case VGGT_TUNE_ATTN_WAVES:
-      if (value != 4 && value != 8) return VGGT_ERR_UNSUPPORTED;
+      if (value != 2 && value != 4 && value != 8) return VGGT_ERR_UNSUPPORTED;
       prev = g_vggt_attn_waves;
       g_vggt_attn_waves = value;
       return prev;

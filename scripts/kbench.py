@@ -107,7 +107,7 @@ def main():
         for rnd, var, nw, (name, batch, n) in [(r_, v_, w_, sh) for r_ in range(args.rounds)
                                           for v_ in map(int, args.attn_variants.split(","))
                                           for w_ in map(int, args.attn_waves.split(","))
-                                          for sh in (("global_attn", 1, M), ("frame_attn", 16, 1374))]:
+                                          for sh in (("global_attn", 1, M), ("frame_attn", 16, M // 16))]:
             N.tune(N.TUNE_ATTN_WAVES, nw)
             N.tune(N.TUNE_ATTN_VARIANT, var)
             us = timeit(lambda: N.attention(q, k, v, o, batch, H, n, n, D, n, n, n),

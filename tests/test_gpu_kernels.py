@@ -284,12 +284,14 @@ def _attention_vs_torch(N, D, H, batch, n):
     assert _rel(o, ref) < 1e-2, _rel(o, ref)
 
 
-@pytest.mark.parametrize("n", [4100, 5000, 8191])
-def test_attention_eight_wave_form(N, n):
-    """8-wave (256-query-row) workgroups, used for nq >= 4096."""
-    prev = N.tune(N.TUNE_ATTN_WAVES, 8)
+@pytest.mark.parametrize("waves,n,D", [(8, 4100, 64), (8, 5000, 64), (8, 8191, 64), (2, 65, 64), (2, 1374, 64),
+                                        (2, 6592, 64), (2, 1375, 128), (2, 33, 128)])
+def test_attention_eight_wave_form(N, waves, n, D):
+    """8-wave (256-query-row) workgroups, used for nq >= 4096, and 2-wave
+    (64-row) workgroups (VGGT_TUNE_ATTN_WAVES 2)."""
+    prev = N.tune(N.TUNE_ATTN_WAVES, waves)
     try:
-        H, D = 2, 64
+        H = 2
         C = H * D
         g = torch.Generator(device="cuda").manual_seed(n)
         qkv = (torch.randn(n, 3 * C, device="cuda", generator=g) * 1.5).to(torch.bfloat16)
