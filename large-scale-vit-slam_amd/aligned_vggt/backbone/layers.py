@@ -178,7 +178,8 @@ class Block(nn.Module):
         hid = ws.buf("blk_h", M, w.shape[0], torch.bfloat16)
         N.gemm_bf16(xn, w, b, hid, N.EPI_GELU_BF16)
         w, b = pack_linear(self.mlp.fc2)
-        if not (_FUSED_ADD_LN and C % 256 == 0 and C <= 2048):
+        # the row pass has kernels for C / 256 in {1, 2, 4, 8} only (norm.hip)
+        if not (_FUSED_ADD_LN and C in (256, 512, 1024, 2048)):
             N.gemm_bf16(hid, w, b, xs, N.EPI_RESID_F32, gamma=self._gamma(self.ls2, C, x.device), out2=out2)
             return False
         # fc2 with a plain bf16 epilogue, then ONE row pass for the LayerScale

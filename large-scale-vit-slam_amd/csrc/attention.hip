@@ -543,7 +543,8 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
   const int nwg = ((nq + nw * 32 - 1) / (nw * 32)) * heads * batch;
   hipStream_t s = (hipStream_t)stream;
   if ((g_vggt_attn_variant == 19 || g_vggt_attn_variant == 23) && D == 64 && nw != 2) {  // pipelined QK^T (3 LDS slots)
-    if (nw == 8) attn_fwd_kernel<64, 8, 19><<<nwg, 512, 0, s>>>(a);
+    if (nw == 8 && g_vggt_attn_variant == 23) attn_fwd_kernel<64, 8, 23><<<nwg, 512, 0, s>>>(a);
+    else if (nw == 8) attn_fwd_kernel<64, 8, 19><<<nwg, 512, 0, s>>>(a);
     else if (g_vggt_attn_variant == 23) attn_fwd_kernel<64, 4, 23><<<nwg, 256, 0, s>>>(a);
     else attn_fwd_kernel<64, 4, 19><<<nwg, 256, 0, s>>>(a);
     HIP_LAUNCH_CHECK();

@@ -284,7 +284,7 @@ def _attention_vs_torch(N, D, H, batch, n):
     assert _rel(o, ref) < 1e-2, _rel(o, ref)
 
 
-@pytest.mark.parametrize("waves,n,D", [(8, 4100, 64), (8, 5000, 64), (8, 8191, 64), (2, 65, 64), (2, 1374, 64),
+@pytest.mark.parametrize("waves,n,D", [(8, 4100, 64), (8, 5000, 64), (8, 8191, 64), (8, 4100, 128), (2, 65, 64), (2, 1374, 64),
                                         (2, 6592, 64), (2, 1375, 128), (2, 33, 128)])
 def test_attention_eight_wave_form(N, waves, n, D):
     """8-wave (256-query-row) workgroups, used for nq >= 4096, and 2-wave
@@ -334,21 +334,23 @@ def test_attention_online_softmax_rescale(N, variant):
 
 @pytest.mark.parametrize("variant", [32, 33, 96, 97])
 @pytest.mark.parametrize("case", ["overflow_late", "all_negative", "huge_first_tile", "mixed_rows"])
-def test_attention_offset_free_extremes(N, variant, case):
+@pytest.mark.parametrize("waves,n", [(4, 700), (8, 4200)])
+def test_attention_offset_free_extremes(N, variant, case, waves, n):
     """Offset-free softmax (VAR & 32): every branch of its range guard against
     an fp64 host reference of the whole tensor (cdna_hip_programming.md §5.4
     rule 26) -- rows whose scores overflow 2^60 only in a late tile, rows whose
     first-tile max is below -60 or above +60 (offset rows), and a mix of offset
-    and zero-offset rows inside one wave."""
-    n, H, D = 700, 2, 64
+    and zero-offset rows inside one wave.  Run on the 4-wave form and on the
+    8-wave form (nq >= 4096, the default there: static priority for waves 4-7)."""
+    H, D = 2, 64
     C = H * D
     g = torch.Generator().manual_seed(7)
     q = torch.randn(n, C, generator=g) * 0.3
     k = torch.randn(n, C, generator=g) * 0.3
     v = torch.randn(n, C, generator=g)
-    if case == "overflow_late":      # score ~ +1100 (log2 units ~ +200) at key 650
+    if case == "overflow_late":      # score ~ +1100 (log2 units ~ +200) at key n - 50
         q[:40] = 4.0
-        k[650] = 4.0
+        k[n - 50] = 4.0
     elif case == "all_negative":     # every score ~ -900 for the first rows
         q[:64] = 4.0
         k[:] = -3.5 + 0.05 * torch.randn(n, C, generator=g)
@@ -357,10 +359,12 @@ def test_attention_offset_free_extremes(N, variant, case):
         k[3] = 4.0
     else:                            # alternate rows: offset / zero-offset in one wave
         q[0:128:2] = 4.0
+        q[n - 256:n - 128:2] = 4.0  # rows of the second half of an 8-wave group
         k[10] = 4.0
-        k[600] = 4.5
+        k[n - 100] = 4.5
     qkv = torch.cat([q, k, v], 1).to(torch.bfloat16)
     prev = N.tune(N.TUNE_ATTN_VARIANT, variant)
+    prev_w = N.tune(N.TUNE_ATTN_WAVES, waves)
     try:
         qkv_d = qkv.cuda()
         o = torch.empty(n, C, device="cuda", dtype=torch.bfloat16)
@@ -368,6 +372,7 @@ def test_attention_offset_free_extremes(N, variant, case):
         torch.cuda.synchronize()
     finally:
         N.tune(N.TUNE_ATTN_VARIANT, prev)
+        N.tune(N.TUNE_ATTN_WAVES, prev_w)
     t = qkv.double().view(1, n, 3, H, D).permute(2, 0, 3, 1, 4)
     ref = _ref_attn(t[0], t[1], t[2], D ** -0.5).permute(0, 2, 1, 3).reshape(n, C)
     got = o.double().cpu()
