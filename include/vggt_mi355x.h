@@ -54,7 +54,9 @@ const char* vggt_version(void);
  * on the variant beyond fp32 summation order inside one MFMA tile. */
 #define VGGT_TUNE_GEMM_TILE 1  /* -1 auto, 0: 128x128 tile, 1: 256x256 ring, 2: 256x128 ring, 3: ping-pong (width by
                                   round quantisation), 4/5/6: ping-pong 256/192/128 wide, 7: ping-pong 256 wide when
-                                  that fills two rounds of CUs, else as 3 */
+                                  that fills two rounds of CUs, else as 3, 8: two-per-CU 256x128 (32x32x16 MFMA),
+                                  9: persistent 256x256 ping-pong with register epilogue (bf16 / GELU / f32
+                                  epilogues, N <= 4096; others as 7) */
 #define VGGT_TUNE_ATTN_WAVES 2 /* 2, 4 or 8 waves (64 / 128 / 256 query rows) per attention workgroup */
 #define VGGT_TUNE_ATTN_VARIANT 3 /* 0-15: attention instruction-schedule variant bits */
 #define VGGT_TUNE_CONV_PF2 4     /* split-bf16 conv gather: 1 two-deep (buffer loads, default), 0 one-deep */

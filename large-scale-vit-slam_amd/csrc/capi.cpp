@@ -24,8 +24,9 @@ extern "C" int vggt_tune(int knob, int value) {
   switch (knob) {
     case VGGT_TUNE_GEMM_TILE:
       // -1 auto, 0 128x128, 1/2 256-row ring (BN 256/128), 3 ping-pong (BN picked), 4/5/6 ping-pong BN 256/192/128,
-      // 7 ping-pong BN 256 when it fills two rounds of CUs, else picked (the auto choice)
-      if (value < -1 || value > 7) return VGGT_ERR_UNSUPPORTED;
+      // 7 ping-pong BN 256 when it fills two rounds of CUs, else picked; 8 two-per-CU 256x128;
+      // 9 persistent ping-pong 256x256 (bf16 / GELU / f32 epilogues, else as 7)
+      if (value < -1 || value > 9) return VGGT_ERR_UNSUPPORTED;
       prev = g_vggt_gemm_tile;
       g_vggt_gemm_tile = value;
       return prev;

@@ -565,6 +565,200 @@ int launch_ring(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int 
 }
 
 // ===========================================================================
+// Two-per-CU form: 256 x 128 block tile, 4 waves (2 M x 2 N; wave tile
+// 128 x 64 = 8 x 4 fragments of v_mfma_f32_16x16x32_bf16), BK = 32, a 3-slot
+// LDS ring filled by LDS-DMA two K-steps ahead behind a counted vmcnt and a
+// raw barrier (one per K-step), fragments double-buffered in registers.
+// __launch_bounds__(256, 2) and 72 KiB of LDS: TWO workgroups per CU, meant
+// to run one workgroup's epilogue beside the other's MFMA main loop.
+// Measured and not used by default (scripts/gemmbench.py, r3c-r3f): the
+// 64-B-row K-steps make its main loop slower than the 256x256 ping-pong
+// form (fc1 plain 193-197 vs 173-179 us), and the epilogue still does not
+// overlap (GELU +37-44 us in both forms), with or without a half-tile start
+// stagger of the second workgroup slot or s_setprio around the MFMAs.
+// ===========================================================================
+constexpr int TBM = 256, TBN = 128, TBK = 32, TNT = 256, TSLOTS = 3;
+
+struct TwoCfg {
+  static constexpr int WN = 2;                    // waves along N
+  static constexpr int TM = 128, TN = 64;         // wave tile
+  static constexpr int MI = TM / 32, NI = TN / 32;  // 32x32 fragments
+  static constexpr int ABYTES = TBM * TBK * 2;    // 16 KiB
+  static constexpr int WBYTES = TBN * TBK * 2;    // 8 KiB
+  static constexpr int SLOT = ABYTES + WBYTES;    // 24 KiB
+  static constexpr int AL = ABYTES / 1024 / 4;    // LDS-DMA instructions per wave per stage (A)
+  static constexpr int WL = WBYTES / 1024 / 4;    // (W)
+  static constexpr int LPS = AL + WL;             // vmcnt units per stage
+  static constexpr int CROW = TBN * 2 + 16;
+  static constexpr int LDS = TSLOTS * SLOT;
+};
+static_assert(TwoCfg::LDS >= TBM * TwoCfg::CROW, "the bf16 C tile reuses the ring");
+static_assert(TwoCfg::LPS == 6, "wait counts below assume 6 DMA instructions per stage");
+
+// The main loop runs on v_mfma_f32_32x32x16_bf16, which holds the SIMD's
+// vector issue for 8 of its 32 cycles (the 16x16x32 form: 8 of 16), so the
+// other workgroup's epilogue VALU finds issue slots beside it.
+template <int EPI>
+__global__ __launch_bounds__(TNT, 2) void gemm_two_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                          const bf16_t* __restrict__ W, int64_t ldw, int M, int N,
+                                                          int K, Epi ep) {
+  using C = TwoCfg;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tiles_n = N / TBN;
+  const int tiles_m = (M + TBM - 1) / TBM;
+  const int ntiles = tiles_m * tiles_n;
+  const int nk = K / TBK;
+  // Persistent: workgroup b runs tiles b, b + grid, ... (all on b's XCD; the
+  // remap keeps each XCD's tiles contiguous in M-panel order).
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem));
+  auto slot_of = [](int kt) -> uint32_t { return (uint32_t)(kt % TSLOTS) * C::SLOT; };
+  // ---- loop-invariant fragment read offsets: fragment row & 31 == lane & 31,
+  // k chunk 2*ks + (lane >> 5) of the 64-B row, swizzled
+  const int wm = wave / C::WN, wn = wave % C::WN;
+  const int fr = lane & 31, hl = lane >> 5;
+  uint32_t a_off[2], w_off[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const uint32_t lo = fr * 64 + (ring_swz(fr, 2 * ks + hl) << 4);
+    a_off[ks] = (wm * C::TM) * 64 + lo;
+    w_off[ks] = C::ABYTES + (wn * C::TN) * 64 + lo;
+  }
+
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int t = xcd_remap(tile, ntiles);
+    const int m0 = (t / tiles_n) * TBM;
+    const int n0 = (t % tiles_n) * TBN;
+
+    // ---- DMA offsets: instruction i of this wave covers rows
+    // (wave*L + i)*16 + lane/4 (64-B rows), source chunk swizzled; rows past M
+    // clamp to M-1.
+    const int32x4 ra = make_rsrc_u(A + (int64_t)m0 * lda);
+    const int32x4 rw = make_rsrc_u(W + (int64_t)n0 * ldw);
+    uint32_t aoff[C::AL], woff[C::WL];
+#pragma unroll
+    for (int i = 0; i < C::AL; ++i) {
+      const int row = (wave * C::AL + i) * 16 + (lane >> 2);
+      const int rr = min(m0 + row, M - 1) - m0;
+      aoff[i] = (uint32_t)(rr * lda + ring_swz(row, lane & 3) * 8) * 2u;
+    }
+#pragma unroll
+    for (int i = 0; i < C::WL; ++i) {
+      const int row = (wave * C::WL + i) * 16 + (lane >> 2);
+      woff[i] = (uint32_t)(row * ldw + ring_swz(row, lane & 3) * 8) * 2u;
+    }
+    auto stage = [&](int kt) {
+      const uint32_t slot = lds0 + slot_of(kt);
+      const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(kt * TBK * 2));
+#pragma unroll
+      for (int i = 0; i < C::AL; ++i) dma16s(ra, aoff[i], soff, slot + (wave * C::AL + i) * 1024);
+#pragma unroll
+      for (int i = 0; i < C::WL; ++i) dma16s(rw, woff[i], soff, slot + C::ABYTES + (wave * C::WL + i) * 1024);
+    };
+
+    f32x16 acc[C::NI][C::MI];
+#pragma unroll
+    for (int i = 0; i < C::NI; ++i)
+#pragma unroll
+      for (int j = 0; j < C::MI; ++j) acc[i][j] = f32x16{};
+
+    // fragments of one 16-deep half K-step, double-buffered per half: the
+    // MFMAs of half h run beside the reads of half h+1
+    struct Frag {
+      bf16x8 w[C::NI], a[C::MI];
+    };
+    auto read_half = [&](int kt, int ks, Frag& f) {
+      const char* base = smem + slot_of(kt);
+#pragma unroll
+      for (int i = 0; i < C::NI; ++i) f.w[i] = *(const bf16x8*)(base + w_off[ks] + i * 32 * 64);
+#pragma unroll
+      for (int i = 0; i < C::MI; ++i) f.a[i] = *(const bf16x8*)(base + a_off[ks] + i * 32 * 64);
+    };
+    auto mfmas = [&](const Frag& f) {
+#pragma unroll
+      for (int mi = 0; mi < C::MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < C::NI; ++ni)
+          acc[ni][mi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.w[ni], f.a[mi], acc[ni][mi], 0, 0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, C::NI + C::MI, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, C::NI * C::MI - 1, 0);
+    };
+    // one K-step on slot kt: half 0 (reads of half 1 beside it), then -- once
+    // every read of slot kt retired and slot kt+1 landed for every wave (slot
+    // kt+2 stays in flight across the barrier) -- restage slot kt with kt+3
+    // and run half 1 beside the reads of the next step's half 0
+    Frag f0, f1;
+    auto step = [&](int kt) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      read_half(kt, 1, f1);
+      mfmas(f0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      if (kt + 3 < nk) stage(kt + 3);  // into slot kt % 3
+      read_half(kt + 1, 0, f0);  // unconditional (a stale slot after the last step, unused)
+      mfmas(f1);
+    };
+
+    stage(0);
+    if (nk > 1) stage(1);
+    if (nk > 2) stage(2);
+    if (nk > 2) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+    else if (nk > 1) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    read_half(0, 0, f0);
+    for (int kt = 0; kt < nk; ++kt) step(kt);
+    // all waves done with the ring (no DMA or read pending): reuse it as the C tile
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+    // ---- epilogue 1: acc (C^T fragments: lane = token, rows 8g + 4hl + 0..3 =
+    // features) + bias -> bf16 C tile in LDS
+    char* Cs = smem;
+#pragma unroll
+    for (int ni = 0; ni < C::NI; ++ni)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int nl = wn * C::TN + ni * 32 + 8 * g + 4 * hl;
+        const f32x4 bv = *(const f32x4*)(ep.bias + n0 + nl);
+#pragma unroll
+        for (int mi = 0; mi < C::MI; ++mi) {
+          const int ml = wm * C::TM + mi * 32 + fr;
+          uint2 pk;
+          pk.x = pack_bf2(acc[ni][mi][4 * g] + bv[0], acc[ni][mi][4 * g + 1] + bv[1]);
+          pk.y = pack_bf2(acc[ni][mi][4 * g + 2] + bv[2], acc[ni][mi][4 * g + 3] + bv[3]);
+          *(uint2*)(Cs + ml * C::CROW + nl * 2) = pk;
+        }
+      }
+    __syncthreads();
+    write_tile<EPI, TBM, TBN, TNT, C::CROW>(Cs, m0, n0, M, ep);
+    __syncthreads();  // the C tile (= the ring) is read out before the next tile's DMA
+  }
+}
+
+template <int EPI>
+int launch_two(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int M, int N, int K, const Epi& ep,
+               hipStream_t s) {
+  static bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)gemm_two_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              TwoCfg::LDS);
+    return true;
+  }();
+  (void)attr;
+  static int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    return n;
+  }();
+  const int ntiles = ((M + TBM - 1) / TBM) * (N / TBN);
+  const int nwg = ntiles < 2 * cus ? ntiles : 2 * cus;
+  gemm_two_kernel<EPI><<<nwg, TNT, TwoCfg::LDS, s>>>(a, lda, w, ldw, M, N, K, ep);
+  return VGGT_OK;
+}
+
+// ===========================================================================
 // Ping-pong form: 256 x BN block tile (BN = 256 / 192 / 128), BK = 64, two
 // LDS buffers filled by LDS-DMA, 8 waves as 2 (M) x 4 (N); wave (wm, wn) owns
 // rows wm*128.. and columns wn*BN/4.. of the tile.  Each K-tile is two
@@ -753,6 +947,251 @@ int launch_pp(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int M,
   return VGGT_OK;
 }
 
+// ===========================================================================
+// Persistent ping-pong form (mode 9): the 256 x 256 ping-pong main loop above,
+// one workgroup per CU looping over tiles, with the epilogue written straight
+// from the accumulators (bias from an LDS copy, GELU, bf16 pack, buffer
+// stores) and the NEXT tile's first two K-tiles issued by LDS-DMA before the
+// epilogue: the operand loads land while the epilogue runs, and the stores
+// drain during the next tile's first K-tile instead of before the workgroup
+// may retire (the one-shot forms pay prologue latency + epilogue + store
+// drain per tile: ~9 us of a ~30 us fc1 tile, scripts/gemmbench.py K=64 runs).
+//
+// vmcnt bookkeeping (gfx9: one in-order counter for loads, stores and
+// LDS-DMA, max 63): per wave a K-tile is LPS = AL + WL DMA pieces and the
+// epilogue issues exactly NST buffer stores (always issued: rows past M are
+// dropped by the descriptor's num_records), so
+//   * after the epilogue: vmcnt(LPS + NST) = this wave's K-tile 0 landed;
+//   * READ(0, 1) of a tile after the first: vmcnt(NST) = K-tile 1 landed;
+//   * every other READ(kt, 1): vmcnt(0) (K-tile kt+1 is the youngest).
+// The bias of all N columns is copied to LDS once (N <= 4096), so the
+// epilogue issues no compiler-visible global load (whose wait would drain
+// the in-flight DMA).
+// ===========================================================================
+constexpr int PP_MAXN = 4096;
+
+template <int EPI>
+__global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                          const bf16_t* __restrict__ W, int64_t ldw, int M, int N,
+                                                          int K, Epi ep) {
+  constexpr int BN = 256;
+  using C = PPCfg<BN>;
+  constexpr int LPS = C::AL + C::WL;
+  constexpr int NST = EPI == VGGT_EPI_F32 ? C::NI * C::MI : C::NI * C::MI / 2;  // buffer stores per wave per tile
+  static_assert(LPS + NST <= 63, "vmcnt range");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* bias_s = (float*)(smem + 2 * C::BUF);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tiles_n = N / BN;
+  const int tiles_m = (M + PBM - 1) / PBM;
+  const int ntiles = tiles_m * tiles_n;
+  const int nk = K / PBK;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  for (int i = threadIdx.x; i < N; i += PNT) bias_s[i] = ep.bias[i];
+  __syncthreads();  // no DMA in flight yet: a plain barrier
+
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem));
+  const int fr = lane & 15, fc = lane >> 4;
+  uint32_t a_off[2], w_off[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const uint32_t sw = (uint32_t)(((ks * 4 + fc) ^ (fr & 7)) << 4);
+    a_off[ks] = (wm * 128 + fr) * 128 + sw;
+    w_off[ks] = C::ABYTES + (wn * C::WN + fr) * 128 + sw;
+  }
+  // per-tile DMA state
+  int32x4 ra, rw;
+  uint32_t aoff[C::AL], woff[C::WL];
+  auto setup = [&](int tile) {
+    const int t = xcd_remap(tile, ntiles);
+    const int m0 = (t / tiles_n) * PBM, n0 = (t % tiles_n) * BN;
+    ra = make_rsrc_u(A + (int64_t)m0 * lda);
+    rw = make_rsrc_u(W + (int64_t)n0 * ldw);
+#pragma unroll
+    for (int i = 0; i < C::AL; ++i) {
+      const int row = (wave * C::AL + i) * 8 + (lane >> 3);
+      const int rr = min(m0 + row, M - 1) - m0;
+      aoff[i] = (uint32_t)(rr * lda + ((lane & 7) ^ (row & 7)) * 8) * 2u;
+    }
+#pragma unroll
+    for (int i = 0; i < C::WL; ++i) {
+      const int row = (wave * C::WL + i) * 8 + (lane >> 3);
+      woff[i] = (uint32_t)(row * ldw + ((lane & 7) ^ (row & 7)) * 8) * 2u;
+    }
+  };
+  auto stage = [&](int buf, int kt) {
+    const uint32_t b = lds0 + buf * C::BUF;
+    const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(kt * PBK * 2));
+#pragma unroll
+    for (int i = 0; i < C::AL; ++i) dma16s(ra, aoff[i], soff, b + (wave * C::AL + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < C::WL; ++i) dma16s(rw, woff[i], soff, b + C::ABYTES + (wave * C::WL + i) * 1024);
+  };
+
+  f32x4 acc[C::NI][C::MI];
+  bf16x8 af[C::MI], wf[C::NI];
+  auto read_frags = [&](int buf, int ks) {
+    const char* base = smem + buf * C::BUF;
+#pragma unroll
+    for (int i = 0; i < C::NI; ++i) wf[i] = *(const bf16x8*)(base + w_off[ks] + i * 16 * 128);
+#pragma unroll
+    for (int i = 0; i < C::MI; ++i) af[i] = *(const bf16x8*)(base + a_off[ks] + i * 16 * 128);
+  };
+  auto math = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mi = 0; mi < C::MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < C::NI; ++ni)
+        acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], af[mi], acc[ni][mi], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  int tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  // prologue: the first tile's K-tiles 0 and 1
+  setup(tile);
+  int b0 = 0;  // buffer of the current tile's K-tile 0
+  stage(0, 0);
+  if (nk > 1) {
+    stage(1, 1);
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(LPS) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  bool stores_out = false;  // this wave has NST epilogue stores younger than K-tile 1's DMA
+  for (;;) {
+    const int t = xcd_remap(tile, ntiles);
+    const int m0 = (t / tiles_n) * PBM, n0 = (t % tiles_n) * BN;
+#pragma unroll
+    for (int i = 0; i < C::NI; ++i)
+#pragma unroll
+      for (int j = 0; j < C::MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (wm == 1) asm volatile("s_barrier" ::: "memory");  // stagger the second M half by one segment
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = (b0 + kt) & 1;
+      // READ(kt, 0): K-tile kt+1's DMA (K-tile 1 was issued ahead), this step's fragments
+      if (kt >= 1 && kt + 1 < nk) stage(buf ^ 1, kt + 1);
+      read_frags(buf, 0);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      math();
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_barrier" ::: "memory");
+      // READ(kt, 1); own DMA of K-tile kt+1 retired before the barrier
+      read_frags(buf, 1);
+      if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NST) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      math();
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_barrier" ::: "memory");
+    }
+    if (wm == 0) asm volatile("s_barrier" ::: "memory");  // balance the stagger
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every read of both buffers retired
+
+    // the next tile's K-tiles 0 and 1, in flight during this epilogue
+    const int next = tile + gridDim.x;
+    const bool more = next < ntiles;
+    const int nb0 = (b0 + nk) & 1;
+    if (more) {
+      setup(next);
+      stage(nb0, 0);
+      if (nk > 1) stage(nb0 ^ 1, 1);
+    }
+
+    // ---- epilogue straight from the accumulators: lane holds features
+    // n..n+3 of token m (C^T fragments).  bf16: fragments ni, ni+1 packed to
+    // 2 dwords each, then one v_permlane16_swap per dword pairs the 16-lane
+    // rows so every lane holds 8 consecutive features (cdna_hip_programming.md
+    // T21, the 16x16 form): one 16-B buffer store per fragment pair.  f32: one
+    // 16-B store per fragment.
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((char*)ep.out + (int64_t)m0 * ep.ldo * (EPI == VGGT_EPI_F32 ? 4 : 2)), 0,
+        (int)(min(M - m0, PBM) * ep.ldo * (EPI == VGGT_EPI_F32 ? 4 : 2)), 0x00020000);
+    typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+    const int rg = lane >> 4;
+    if constexpr (EPI == VGGT_EPI_F32) {
+#pragma unroll
+      for (int ni = 0; ni < C::NI; ++ni) {
+        const int nl = n0 + wn * C::WN + ni * 16 + 4 * rg;
+        const f32x4 bv = *(const f32x4*)(bias_s + nl);
+#pragma unroll
+        for (int mi = 0; mi < C::MI; ++mi) {
+          const int ml = wm * 128 + mi * 16 + (lane & 15);
+          f32x4 v = acc[ni][mi] + bv;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = round_bf(v[j]);  // the reference's bf16 Linear output, widened
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ro, (ml * (int)ep.ldo + nl) * 4, 0, 0);
+        }
+      }
+    } else {
+      // after the swap, row group rg holds fragment ni + (rg & 1), features 8 * (rg >> 1) ..
+      const int ncol = (rg & 1) * 16 + (rg >> 1) * 8;
+#pragma unroll
+      for (int np = 0; np < C::NI; np += 2) {
+        const f32x4 bv0 = *(const f32x4*)(bias_s + n0 + wn * C::WN + np * 16 + 4 * rg);
+        const f32x4 bv1 = *(const f32x4*)(bias_s + n0 + wn * C::WN + (np + 1) * 16 + 4 * rg);
+        const int nl = n0 + wn * C::WN + np * 16 + ncol;
+#pragma unroll
+        for (int mi = 0; mi < C::MI; ++mi) {
+          const int ml = wm * 128 + mi * 16 + (lane & 15);
+          f32x4 v0 = acc[np][mi] + bv0, v1 = acc[np + 1][mi] + bv1;
+          if constexpr (EPI == VGGT_EPI_GELU_BF16) {
+            // GELU of the bf16-rounded Linear output (autocast), rounded to bf16
+            const f32x2 g0 = gelu_fast2(f32x2{round_bf(v0[0]), round_bf(v0[1])});
+            const f32x2 g1 = gelu_fast2(f32x2{round_bf(v0[2]), round_bf(v0[3])});
+            const f32x2 g2 = gelu_fast2(f32x2{round_bf(v1[0]), round_bf(v1[1])});
+            const f32x2 g3 = gelu_fast2(f32x2{round_bf(v1[2]), round_bf(v1[3])});
+            v0 = f32x4{g0[0], g0[1], g1[0], g1[1]};
+            v1 = f32x4{g2[0], g2[1], g3[0], g3[1]};
+          }
+          uint32_t a0 = pack_bf2(v0[0], v0[1]), a1 = pack_bf2(v0[2], v0[3]);
+          uint32_t b0 = pack_bf2(v1[0], v1[1]), b1 = pack_bf2(v1[2], v1[3]);
+          // rows 1 <-> 0 and 3 <-> 2 of (a = fragment np, b = fragment np+1)
+          const auto s0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+          const u32x4 pk = {s0[0], s1[0], s0[1], s1[1]};
+          __builtin_amdgcn_raw_buffer_store_b128(pk, ro, (ml * (int)ep.ldo + nl) * 2, 0, 0);
+        }
+      }
+    }
+    if (!more) break;
+    // own K-tile 0 of the next tile landed (K-tile 1 and the stores may still
+    // be in flight), then everyone's
+    if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(LPS + NST) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NST) : "memory");
+    stores_out = true;
+    tile = next;
+    b0 = nb0;
+  }
+}
+
+template <int EPI>
+int launch_ppp(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int M, int N, int K, const Epi& ep,
+               hipStream_t s) {
+  using C = PPCfg<256>;
+  constexpr int LDS = 2 * C::BUF + PP_MAXN * 4;
+  static bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)gemm_ppp_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    return true;
+  }();
+  (void)attr;
+  static int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    return n;
+  }();
+  const int ntiles = ((M + PBM - 1) / PBM) * (N / 256);
+  // a multiple of 8 workgroups keeps every workgroup's tiles on its own XCD
+  const int nwg = ntiles < cus ? ntiles : cus;
+  gemm_ppp_kernel<EPI><<<nwg, PNT, LDS, s>>>(a, lda, w, ldw, M, N, K, ep);
+  return VGGT_OK;
+}
+
 // Ping-pong tile width for an N-wide output: the BN whose whole rounds of
 // 256-row tiles over the CUs cost least (per-tile time ~ BN), larger BN on a
 // tie; 192 only where the epilogue allows it.
@@ -824,11 +1263,40 @@ int gemm_impl(const void* A, int64_t lda, const void* W, int64_t ldw, const floa
   int mode = g_vggt_gemm_tile;
   if (mode < 0)
     mode = (M >= 4096 && K % PBK == 0 && N % 256 == 0 && N >= 2048 && epi != VGGT_EPI_RESID_F32) ? 7 : 0;
-  if (mode >= 3 && K % PBK) mode = 2;    // the ping-pong form steps K by 64
+  // auto: the persistent ping-pong form where 256x256 tiles fill several
+  // rounds of CUs (the 16x518^2 chunk: fc1 + GELU 217 -> 204 us, plain qkv
+  // shape 159 -> 139 us, scripts/gemmbench.py r3i); it falls back to mode 7
+  // for the epilogues it does not cover
+  if (g_vggt_gemm_tile < 0 && mode == 7 && M >= 16384 && N <= PP_MAXN) mode = 9;
+  if (mode >= 3 && mode <= 7 && K % PBK) mode = 2;    // the ping-pong form steps K by 64
   if (mode == 0 && K % BK) mode = 2;     // the 128x128 form steps K by 64
   if (mode == 1 && N % 256) mode = 2;
   // per-lane 32-bit DMA offsets span one 256-row panel
   if (mode != 0 && (int64_t)RBM * (lda > ldw ? lda : ldw) * 2 >= (1ll << 31)) return VGGT_ERR_SHAPE;
+  if (mode == 9 && (N % 256 || N > PP_MAXN || K % PBK || epi == VGGT_EPI_RESID_F32 || out2 ||
+                    (int64_t)PBM * (ldo > 0 ? ldo : 1) * 4 >= (1ll << 31)))
+    mode = K % PBK ? 2 : 7;  // the persistent form covers the bf16 / GELU / f32 epilogues up to N = 4096
+  if (mode == 9) {
+    switch (epi) {
+      case VGGT_EPI_BF16: launch_ppp<VGGT_EPI_BF16>(a, lda, w, ldw, M, N, K, ep, s); break;
+      case VGGT_EPI_GELU_BF16: launch_ppp<VGGT_EPI_GELU_BF16>(a, lda, w, ldw, M, N, K, ep, s); break;
+      case VGGT_EPI_F32: launch_ppp<VGGT_EPI_F32>(a, lda, w, ldw, M, N, K, ep, s); break;
+      default: return VGGT_ERR_UNSUPPORTED;
+    }
+    HIP_LAUNCH_CHECK();
+    return VGGT_OK;
+  }
+  if (mode == 8) {
+    switch (epi) {
+      case VGGT_EPI_BF16: launch_two<VGGT_EPI_BF16>(a, lda, w, ldw, M, N, K, ep, s); break;
+      case VGGT_EPI_GELU_BF16: launch_two<VGGT_EPI_GELU_BF16>(a, lda, w, ldw, M, N, K, ep, s); break;
+      case VGGT_EPI_RESID_F32: launch_two<VGGT_EPI_RESID_F32>(a, lda, w, ldw, M, N, K, ep, s); break;
+      case VGGT_EPI_F32: launch_two<VGGT_EPI_F32>(a, lda, w, ldw, M, N, K, ep, s); break;
+      default: return VGGT_ERR_UNSUPPORTED;
+    }
+    HIP_LAUNCH_CHECK();
+    return VGGT_OK;
+  }
   if (mode >= 3) {
     int bn = mode == 4 ? 256 : mode == 5 ? 192 : mode == 6 ? 128 : mode == 7 ? pp_auto_bn(M, N, true) : pp_pick_bn(M, N, true);
     if (bn == 0 || N % bn) bn = pp_pick_bn(M, N, true);
@@ -917,10 +1385,16 @@ extern "C" int vggt_gemm_qkv(const void* A, int64_t lda, const void* W, int64_t 
   // 128x128 form, r1s), the 128x128 form otherwise
   int mode = g_vggt_gemm_tile;
   if (mode < 0) mode = (M >= 4096 && K % PBK == 0) ? (N % 256 == 0 ? 7 : 6) : 0;
-  if (mode >= 3 && K % PBK) mode = 2;
+  if (mode >= 3 && mode <= 7 && K % PBK) mode = 2;
   if (mode == 0 && K % BK) mode = 2;
   if (mode == 1 && hd % 256) mode = 2;
   if (mode != 0 && (int64_t)RBM * (lda > ldw ? lda : ldw) * 2 >= (1ll << 31)) return VGGT_ERR_SHAPE;
+  if (mode == 8) {
+    if (D == 64) launch_two<EPI_QKNORM_D64>(a, lda, w, ldw, M, N, K, ep, s);
+    else launch_two<EPI_QKNORM_D128>(a, lda, w, ldw, M, N, K, ep, s);
+    HIP_LAUNCH_CHECK();
+    return VGGT_OK;
+  }
   if (mode >= 3) {
     // 192-wide tiles only with 64-wide heads (the norm's lane groups stay aligned)
     int bn = mode == 4 ? 256 : mode == 5 ? 192 : mode == 6 ? 128 : mode == 7 ? pp_auto_bn(M, N, D == 64) : pp_pick_bn(M, N, D == 64);

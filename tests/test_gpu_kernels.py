@@ -65,7 +65,7 @@ def test_gemm_epilogues(N, M, Nn, K, epi):
         assert _rel(out, refb) < 4e-3
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("M,Nn,K", [(300, 256, 96), (1000, 768, 1024), (2300, 1024, 4096), (21984, 1024, 1024),
                                     (5000, 3072, 1024)])
 @pytest.mark.parametrize("epi", [0, 1, 2])
@@ -399,7 +399,7 @@ def _online_softmax_rescale(N):
     assert _rel(o, ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("D,H,mode,norm", [(64, 16, 1, True), (64, 16, 0, True), (128, 8, 1, True), (128, 8, 2, True),
                                            (64, 4, 1, False)])
 def test_gemm_qkv_fused_matches_two_pass(N, tile, D, H, mode, norm):
@@ -415,11 +415,13 @@ def test_gemm_qkv_fused_production_rows(N, D, H, mode):
     _qkv_fused_check(N, -1, D, H, mode, True, 21984, 1024)
 
 
-@pytest.mark.parametrize("Nn,epi", [(3072, 0), (4096, 1), (4096, 0), (3072, 2), (3072, 3)])
-def test_gemm_production_rows(N, Nn, epi):
-    """Every epilogue at M = 21984 on the 256x256 ping-pong form (86 x 12 or
-    86 x 16 tiles: a partial last round of workgroups, ragged last panel)."""
-    prev = N.tune(N.TUNE_GEMM_TILE, 4)
+@pytest.mark.parametrize("tile", [4, 8, 9])
+@pytest.mark.parametrize("Nn,epi", [(3072, 0), (4096, 1), (4096, 0), (3072, 2), (3072, 3), (1024, 2)])
+def test_gemm_production_rows(N, Nn, epi, tile):
+    """Every epilogue at M = 21984 on the 256x256 ping-pong form and the
+    two-per-CU 256x128 form (a partial last round of workgroups, ragged last
+    panel)."""
+    prev = N.tune(N.TUNE_GEMM_TILE, tile)
     try:
         test_gemm_epilogues(N, 21984, Nn, 1024, epi)
     finally:
