@@ -969,6 +969,24 @@ int launch_pp(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int M,
 // the in-flight DMA).
 // ===========================================================================
 constexpr int PP_MAXN = 4096;
+constexpr int PP_LDS_MAX = 160 * 1024;
+// VGGT_GEMM_PERSIST (A/B of the auto policy): bit 0 = the persistent form for
+// the bf16 / GELU / f32 GEMMs, bit 1 = for the fused qkv GEMM (default both)
+inline int persist_policy() {
+  static int p = [] {
+    const char* e = getenv("VGGT_GEMM_PERSIST");
+    return e ? atoi(e) : 3;
+  }();
+  return p;
+}
+
+// sum over the four 16-lane rows of a wave (lanes l, l^16, l^32, l^48)
+__device__ __forceinline__ float rows4_sum(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
 
 template <int EPI>
 __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restrict__ A, int64_t lda,
@@ -991,6 +1009,30 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
   const int wm = wave >> 2, wn = wave & 3;
 
   for (int i = threadIdx.x; i < N; i += PNT) bias_s[i] = ep.bias[i];
+  // EPI_QKNORM_D64: q/k norm weights (qw qb kw kb, 64 each), RoPE-2D cos / sin
+  // tables [tab_len][32] and the positions (y | x << 8 per position index)
+  float* qkn_s = bias_s + N;
+  float* cs_s = qkn_s + 256;
+  const int tab = (EPI == EPI_QKNORM_D64 && ep.rope_mode == VGGT_ROPE_2D) ? ep.tab_len : 0;
+  float* sn_s = cs_s + tab * 32;
+  uint16_t* pos_s = (uint16_t*)(sn_s + tab * 32);
+  if constexpr (EPI == EPI_QKNORM_D64) {
+    for (int i = threadIdx.x; i < 64; i += PNT) {
+      qkn_s[i] = ep.qw ? ep.qw[i] : 1.f;
+      qkn_s[64 + i] = ep.qb ? ep.qb[i] : 0.f;
+      qkn_s[128 + i] = ep.kw ? ep.kw[i] : 1.f;
+      qkn_s[192 + i] = ep.kb ? ep.kb[i] : 0.f;
+    }
+    for (int i = threadIdx.x; i < tab * 32; i += PNT) {
+      cs_s[i] = ep.cs[i];
+      sn_s[i] = ep.sn[i];
+    }
+    if (tab)
+      for (int i = threadIdx.x; i < ep.period; i += PNT) {
+        const int py = min(max(ep.pos[2 * i], 0), tab - 1), px = min(max(ep.pos[2 * i + 1], 0), tab - 1);
+        pos_s[i] = (uint16_t)(py | (px << 8));
+      }
+  }
   __syncthreads();  // no DMA in flight yet: a plain barrier
 
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem));
@@ -1128,6 +1170,78 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ro, (ml * (int)ep.ldo + nl) * 4, 0, 0);
         }
       }
+    } else if (EPI == EPI_QKNORM_D64 && (n0 + wn * C::WN) / ep.hd < 2) {
+      // q or k head (this wave's 64 columns = one head): fp32 LayerNorm over the
+      // head's 64 bf16 Linear outputs (lane: 16 of them, the rest in lanes
+      // +-16 / +-32 of the same token) then RoPE-2D (y rotates features 0-31,
+      // x 32-63; rotate_half partners e, e+16 are fragments ni, ni+1 of the
+      // same lane), one bf16 rounding -- the arithmetic of headnorm_rope_kernel
+      const int hb = n0 + wn * C::WN;
+      const int region = hb / ep.hd;
+      const bool norm = region ? ep.kw != nullptr : ep.qw != nullptr;
+      f32x4 lw[C::NI], lb[C::NI], bv[C::NI];
+#pragma unroll
+      for (int ni = 0; ni < C::NI; ++ni) {
+        const int e = ni * 16 + 4 * rg;
+        lw[ni] = *(const f32x4*)(qkn_s + region * 128 + e);
+        lb[ni] = *(const f32x4*)(qkn_s + region * 128 + 64 + e);
+        bv[ni] = *(const f32x4*)(bias_s + hb + e);
+      }
+      const int ncol = (rg & 1) * 16 + (rg >> 1) * 8;
+#pragma unroll
+      for (int mi = 0; mi < C::MI; ++mi) {
+        const int ml = wm * 128 + mi * 16 + (lane & 15);
+        f32x4 x[C::NI];
+#pragma unroll
+        for (int ni = 0; ni < C::NI; ++ni) {
+          x[ni] = acc[ni][mi] + bv[ni];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) x[ni][j] = round_bf(x[ni][j]);
+        }
+        if (norm) {
+          float sm = 0.f;
+#pragma unroll
+          for (int ni = 0; ni < C::NI; ++ni) sm += (x[ni][0] + x[ni][1]) + (x[ni][2] + x[ni][3]);
+          const float mean = rows4_sum(sm) * (1.f / 64);
+          float q = 0.f;
+#pragma unroll
+          for (int ni = 0; ni < C::NI; ++ni)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float d = x[ni][j] - mean;
+              q += d * d;
+            }
+          const float rstd = rsqrtf(rows4_sum(q) * (1.f / 64) + ep.eps);
+#pragma unroll
+          for (int ni = 0; ni < C::NI; ++ni)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[ni][j] = (x[ni][j] - mean) * rstd * lw[ni][j] + lb[ni][j];
+        }
+        if (tab) {
+          const int pr = (m0 + ml) % ep.period;
+          const uint32_t pc = pos_s[pr];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {  // h 0: y rotates ni 0/1, h 1: x rotates ni 2/3
+            const int pp = h ? (int)(pc >> 8) : (int)(pc & 255);
+            const float* cp = cs_s + pp * 32 + 4 * rg;
+            const float* sp = sn_s + pp * 32 + 4 * rg;
+            const f32x4 c0 = *(const f32x4*)cp, c1 = *(const f32x4*)(cp + 16);
+            const f32x4 s0 = *(const f32x4*)sp, s1 = *(const f32x4*)(sp + 16);
+            const f32x4 a = x[2 * h], b = x[2 * h + 1];
+            x[2 * h] = a * c0 - b * s0;
+            x[2 * h + 1] = b * c1 + a * s1;
+          }
+        }
+#pragma unroll
+        for (int np = 0; np < C::NI; np += 2) {
+          const uint32_t a0 = pack_bf2(x[np][0], x[np][1]), a1 = pack_bf2(x[np][2], x[np][3]);
+          const uint32_t b0 = pack_bf2(x[np + 1][0], x[np + 1][1]), b1 = pack_bf2(x[np + 1][2], x[np + 1][3]);
+          const auto s0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+          const u32x4 pk = {s0[0], s1[0], s0[1], s1[1]};
+          __builtin_amdgcn_raw_buffer_store_b128(pk, ro, (ml * (int)ep.ldo + hb + np * 16 + ncol) * 2, 0, 0);
+        }
+      }
     } else {
       // after the swap, row group rg holds fragment ni + (rg & 1), features 8 * (rg >> 1) ..
       const int ncol = (rg & 1) * 16 + (rg >> 1) * 8;
@@ -1170,13 +1284,24 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
   }
 }
 
+// LDS bytes of the persistent form: two K-tile buffers, the bias, and for
+// the fused q/k norm + RoPE epilogue its parameters and tables; 0 = does not fit
+inline int ppp_lds_bytes(int epi, int N, const Epi& ep) {
+  using C = PPCfg<256>;
+  int64_t b = 2 * C::BUF + (int64_t)N * 4;
+  if (epi == EPI_QKNORM_D64) {
+    b += 256 * 4;
+    if (ep.rope_mode == VGGT_ROPE_2D) b += 2 * (int64_t)ep.tab_len * 32 * 4 + (((int64_t)ep.period * 2 + 15) & ~15);
+  }
+  return b <= PP_LDS_MAX ? (int)b : 0;
+}
+
 template <int EPI>
 int launch_ppp(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int M, int N, int K, const Epi& ep,
                hipStream_t s) {
-  using C = PPCfg<256>;
-  constexpr int LDS = 2 * C::BUF + PP_MAXN * 4;
   static bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)gemm_ppp_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_ppp_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              PP_LDS_MAX);
     return true;
   }();
   (void)attr;
@@ -1185,10 +1310,11 @@ int launch_ppp(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int M
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
     return n;
   }();
+  const int lds = ppp_lds_bytes(EPI, N, ep);
+  if (!lds) return VGGT_ERR_SHAPE;
   const int ntiles = ((M + PBM - 1) / PBM) * (N / 256);
-  // a multiple of 8 workgroups keeps every workgroup's tiles on its own XCD
   const int nwg = ntiles < cus ? ntiles : cus;
-  gemm_ppp_kernel<EPI><<<nwg, PNT, LDS, s>>>(a, lda, w, ldw, M, N, K, ep);
+  gemm_ppp_kernel<EPI><<<nwg, PNT, lds, s>>>(a, lda, w, ldw, M, N, K, ep);
   return VGGT_OK;
 }
 
@@ -1267,7 +1393,7 @@ int gemm_impl(const void* A, int64_t lda, const void* W, int64_t ldw, const floa
   // rounds of CUs (the 16x518^2 chunk: fc1 + GELU 217 -> 204 us, plain qkv
   // shape 159 -> 139 us, scripts/gemmbench.py r3i); it falls back to mode 7
   // for the epilogues it does not cover
-  if (g_vggt_gemm_tile < 0 && mode == 7 && M >= 16384 && N <= PP_MAXN) mode = 9;
+  if (g_vggt_gemm_tile < 0 && mode == 7 && M >= 16384 && N <= PP_MAXN && (persist_policy() & 1)) mode = 9;
   if (mode >= 3 && mode <= 7 && K % PBK) mode = 2;    // the ping-pong form steps K by 64
   if (mode == 0 && K % BK) mode = 2;     // the 128x128 form steps K by 64
   if (mode == 1 && N % 256) mode = 2;
@@ -1389,6 +1515,22 @@ extern "C" int vggt_gemm_qkv(const void* A, int64_t lda, const void* W, int64_t 
   if (mode == 0 && K % BK) mode = 2;
   if (mode == 1 && hd % 256) mode = 2;
   if (mode != 0 && (int64_t)RBM * (lda > ldw ? lda : ldw) * 2 >= (1ll << 31)) return VGGT_ERR_SHAPE;
+  // auto: the persistent form on the chunk shapes (D = 64 heads, RoPE-2D or none)
+  if (g_vggt_gemm_tile < 0 && mode == 7 && M >= 16384 && (persist_policy() & 2)) mode = 9;
+  if (mode == 9) {
+    bool ok = D == 64 && N % 256 == 0 && N <= PP_MAXN && K % PBK == 0 && rope_mode != VGGT_ROPE_1D &&
+              (int64_t)PBM * ldo * 2 < (1ll << 31) && ppp_lds_bytes(EPI_QKNORM_D64, N, ep) > 0;
+    if (ok && rope_mode == VGGT_ROPE_2D) {
+      // positions are staged as bytes; tables of at most 256 positions
+      ok = tab_len <= 256;
+    }
+    if (ok) {
+      launch_ppp<EPI_QKNORM_D64>(a, lda, w, ldw, M, N, K, ep, s);
+      HIP_LAUNCH_CHECK();
+      return VGGT_OK;
+    }
+    mode = K % PBK ? 2 : 7;
+  }
   if (mode == 8) {
     if (D == 64) launch_two<EPI_QKNORM_D64>(a, lda, w, ldw, M, N, K, ep, s);
     else launch_two<EPI_QKNORM_D128>(a, lda, w, ldw, M, N, K, ep, s);

@@ -399,7 +399,7 @@ def _online_softmax_rescale(N):
     assert _rel(o, ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("D,H,mode,norm", [(64, 16, 1, True), (64, 16, 0, True), (128, 8, 1, True), (128, 8, 2, True),
                                            (64, 4, 1, False)])
 def test_gemm_qkv_fused_matches_two_pass(N, tile, D, H, mode, norm):
