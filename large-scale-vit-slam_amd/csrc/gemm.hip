@@ -971,11 +971,12 @@ int launch_pp(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int M,
 constexpr int PP_MAXN = 4096;
 constexpr int PP_LDS_MAX = 160 * 1024;
 // VGGT_GEMM_PERSIST (A/B of the auto policy): bit 0 = the persistent form for
-// the bf16 / GELU / f32 GEMMs, bit 1 = for the fused qkv GEMM (default both)
+// the bf16 / GELU / f32 GEMMs, bit 1 = for the fused qkv GEMM, bit 2 = for the
+// LayerScale-residual GEMMs (default all)
 inline int persist_policy() {
   static int p = [] {
     const char* e = getenv("VGGT_GEMM_PERSIST");
-    return e ? atoi(e) : 3;
+    return e ? atoi(e) : 7;
   }();
   return p;
 }
@@ -988,27 +989,46 @@ __device__ __forceinline__ float rows4_sum(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
-template <int EPI>
+// Tile BMT x 256 (BMT = 256, or 192 where 256-row tiles quantise badly: the
+// N = 1024 projections, 344 -> 460 tiles on 256 CUs); wave tile (BMT/2) x 64.
+template <int BMT>
+struct PPXCfg {
+  static constexpr int BN = 256, WN = 64, NI = 4, MI = BMT / 32, HM = BMT / 2;
+  static constexpr int ABYTES = BMT * PBK * 2;
+  static constexpr int WBYTES = BN * PBK * 2;
+  static constexpr int BUF = ABYTES + WBYTES;
+  static constexpr int AL = ABYTES / 1024 / 8;
+  static constexpr int WL = WBYTES / 1024 / 8;
+};
+
+template <int EPI, int BMT>
 __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                           const bf16_t* __restrict__ W, int64_t ldw, int M, int N,
                                                           int K, Epi ep) {
   constexpr int BN = 256;
-  using C = PPCfg<BN>;
+  using C = PPXCfg<BMT>;
+  static_assert(C::AL * 1024 * 8 == C::ABYTES, "whole DMA pieces per wave");
   constexpr int LPS = C::AL + C::WL;
-  constexpr int NST = EPI == VGGT_EPI_F32 ? C::NI * C::MI : C::NI * C::MI / 2;  // buffer stores per wave per tile
+  // buffer stores per wave per tile (RESID: the residual and its optional mirror)
+  constexpr int NST = EPI == VGGT_EPI_F32 ? C::NI * C::MI
+                      : EPI == VGGT_EPI_RESID_F32 ? 2 * C::NI * C::MI : C::NI * C::MI / 2;
   static_assert(LPS + NST <= 63, "vmcnt range");
+  static_assert(EPI != VGGT_EPI_RESID_F32 || BMT == 192, "residual tiles are 192 rows (register budget)");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* bias_s = (float*)(smem + 2 * C::BUF);
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tiles_n = N / BN;
-  const int tiles_m = (M + PBM - 1) / PBM;
+  const int tiles_m = (M + BMT - 1) / BMT;
   const int ntiles = tiles_m * tiles_n;
   const int nk = K / PBK;
   const int wm = wave >> 2, wn = wave & 3;
 
   for (int i = threadIdx.x; i < N; i += PNT) bias_s[i] = ep.bias[i];
+  float* gam_s = bias_s + N;  // RESID: LayerScale gamma
+  if constexpr (EPI == VGGT_EPI_RESID_F32)
+    for (int i = threadIdx.x; i < N; i += PNT) gam_s[i] = ep.gamma[i];
   // EPI_QKNORM_D64: q/k norm weights (qw qb kw kb, 64 each), RoPE-2D cos / sin
   // tables [tab_len][32] and the positions (y | x << 8 per position index)
   float* qkn_s = bias_s + N;
@@ -1041,7 +1061,7 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
     const uint32_t sw = (uint32_t)(((ks * 4 + fc) ^ (fr & 7)) << 4);
-    a_off[ks] = (wm * 128 + fr) * 128 + sw;
+    a_off[ks] = (wm * C::HM + fr) * 128 + sw;
     w_off[ks] = C::ABYTES + (wn * C::WN + fr) * 128 + sw;
   }
   // per-tile DMA state
@@ -1049,7 +1069,7 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
   uint32_t aoff[C::AL], woff[C::WL];
   auto setup = [&](int tile) {
     const int t = xcd_remap(tile, ntiles);
-    const int m0 = (t / tiles_n) * PBM, n0 = (t % tiles_n) * BN;
+    const int m0 = (t / tiles_n) * BMT, n0 = (t % tiles_n) * BN;
     ra = make_rsrc_u(A + (int64_t)m0 * lda);
     rw = make_rsrc_u(W + (int64_t)n0 * ldw);
 #pragma unroll
@@ -1107,7 +1127,7 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
   bool stores_out = false;  // this wave has NST epilogue stores younger than K-tile 1's DMA
   for (;;) {
     const int t = xcd_remap(tile, ntiles);
-    const int m0 = (t / tiles_n) * PBM, n0 = (t % tiles_n) * BN;
+    const int m0 = (t / tiles_n) * BMT, n0 = (t % tiles_n) * BN;
 #pragma unroll
     for (int i = 0; i < C::NI; ++i)
 #pragma unroll
@@ -1135,6 +1155,21 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
     if (wm == 0) asm volatile("s_barrier" ::: "memory");  // balance the stagger
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every read of both buffers retired
 
+    // RESID: this tile's fp32 residual rows, loaded BEFORE the next tile's DMA
+    // (the compiler's waits for them then never cover the younger DMA)
+    f32x4 rx[C::NI][EPI == VGGT_EPI_RESID_F32 ? C::MI : 1];
+    if constexpr (EPI == VGGT_EPI_RESID_F32) {
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)((float*)ep.out + (int64_t)m0 * ep.ldo), 0, (int)(min(M - m0, BMT) * ep.ldo * 4), 0x00020000);
+#pragma unroll
+      for (int ni = 0; ni < C::NI; ++ni)
+#pragma unroll
+        for (int mi = 0; mi < C::MI; ++mi) {
+          const int ml = wm * C::HM + mi * 16 + (lane & 15);
+          const int nl = n0 + wn * C::WN + ni * 16 + 4 * (lane >> 4);
+          rx[ni][mi] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, (ml * (int)ep.ldo + nl) * 4, 0, 0));
+        }
+    }
     // the next tile's K-tiles 0 and 1, in flight during this epilogue
     const int next = tile + gridDim.x;
     const bool more = next < ntiles;
@@ -1151,19 +1186,43 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
     // rows so every lane holds 8 consecutive features (cdna_hip_programming.md
     // T21, the 16x16 form): one 16-B buffer store per fragment pair.  f32: one
     // 16-B store per fragment.
+    constexpr int OB = (EPI == VGGT_EPI_F32 || EPI == VGGT_EPI_RESID_F32) ? 4 : 2;  // output element bytes
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((char*)ep.out + (int64_t)m0 * ep.ldo * (EPI == VGGT_EPI_F32 ? 4 : 2)), 0,
-        (int)(min(M - m0, PBM) * ep.ldo * (EPI == VGGT_EPI_F32 ? 4 : 2)), 0x00020000);
+        (void*)((char*)ep.out + (int64_t)m0 * ep.ldo * OB), 0, (int)(min(M - m0, BMT) * ep.ldo * OB), 0x00020000);
     typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
     const int rg = lane >> 4;
-    if constexpr (EPI == VGGT_EPI_F32) {
+    if constexpr (EPI == VGGT_EPI_RESID_F32) {
+      // x += gamma * bf16(acc + bias) (LayerScale on the bf16 Linear output,
+      // fp32 residual), mirrored into out2 (the kept-layer concat) -- with no
+      // out2 the mirror stores go to an empty descriptor and are dropped, so
+      // the store count stays NST
+      const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc(
+          ep.out2 ? (void*)(ep.out2 + (int64_t)m0 * ep.ldo2) : ep.out, 0,
+          ep.out2 ? (int)(min(M - m0, BMT) * ep.ldo2 * 4) : 0, 0x00020000);
+#pragma unroll
+      for (int ni = 0; ni < C::NI; ++ni) {
+        const int nl = n0 + wn * C::WN + ni * 16 + 4 * rg;
+        const f32x4 bv = *(const f32x4*)(bias_s + nl);
+        const f32x4 gv = *(const f32x4*)(gam_s + nl);
+#pragma unroll
+        for (int mi = 0; mi < C::MI; ++mi) {
+          const int ml = wm * C::HM + mi * 16 + (lane & 15);
+          const f32x4 v = acc[ni][mi] + bv;
+          f32x4 x = rx[ni][mi];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) x[j] += gv[j] * round_bf(v[j]);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), ro, (ml * (int)ep.ldo + nl) * 4, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), r2, (ml * (int)ep.ldo2 + nl) * 4, 0, 0);
+        }
+      }
+    } else if constexpr (EPI == VGGT_EPI_F32) {
 #pragma unroll
       for (int ni = 0; ni < C::NI; ++ni) {
         const int nl = n0 + wn * C::WN + ni * 16 + 4 * rg;
         const f32x4 bv = *(const f32x4*)(bias_s + nl);
 #pragma unroll
         for (int mi = 0; mi < C::MI; ++mi) {
-          const int ml = wm * 128 + mi * 16 + (lane & 15);
+          const int ml = wm * C::HM + mi * 16 + (lane & 15);
           f32x4 v = acc[ni][mi] + bv;
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] = round_bf(v[j]);  // the reference's bf16 Linear output, widened
@@ -1190,7 +1249,7 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
       const int ncol = (rg & 1) * 16 + (rg >> 1) * 8;
 #pragma unroll
       for (int mi = 0; mi < C::MI; ++mi) {
-        const int ml = wm * 128 + mi * 16 + (lane & 15);
+        const int ml = wm * C::HM + mi * 16 + (lane & 15);
         f32x4 x[C::NI];
 #pragma unroll
         for (int ni = 0; ni < C::NI; ++ni) {
@@ -1252,7 +1311,7 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
         const int nl = n0 + wn * C::WN + np * 16 + ncol;
 #pragma unroll
         for (int mi = 0; mi < C::MI; ++mi) {
-          const int ml = wm * 128 + mi * 16 + (lane & 15);
+          const int ml = wm * C::HM + mi * 16 + (lane & 15);
           f32x4 v0 = acc[np][mi] + bv0, v1 = acc[np + 1][mi] + bv1;
           if constexpr (EPI == VGGT_EPI_GELU_BF16) {
             // GELU of the bf16-rounded Linear output (autocast), rounded to bf16
@@ -1284,11 +1343,12 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
   }
 }
 
-// LDS bytes of the persistent form: two K-tile buffers, the bias, and for
-// the fused q/k norm + RoPE epilogue its parameters and tables; 0 = does not fit
-inline int ppp_lds_bytes(int epi, int N, const Epi& ep) {
-  using C = PPCfg<256>;
-  int64_t b = 2 * C::BUF + (int64_t)N * 4;
+// LDS bytes of the persistent form: two K-tile buffers, the bias (and the
+// LayerScale gamma), and for the fused q/k norm + RoPE epilogue its parameters
+// and tables; 0 = does not fit
+inline int ppp_lds_bytes(int epi, int bmt, int N, const Epi& ep) {
+  int64_t b = 2 * ((int64_t)bmt * PBK * 2 + 256 * PBK * 2) + (int64_t)N * 4;
+  if (epi == VGGT_EPI_RESID_F32) b += (int64_t)N * 4;
   if (epi == EPI_QKNORM_D64) {
     b += 256 * 4;
     if (ep.rope_mode == VGGT_ROPE_2D) b += 2 * (int64_t)ep.tab_len * 32 * 4 + (((int64_t)ep.period * 2 + 15) & ~15);
@@ -1296,26 +1356,58 @@ inline int ppp_lds_bytes(int epi, int N, const Epi& ep) {
   return b <= PP_LDS_MAX ? (int)b : 0;
 }
 
-template <int EPI>
-int launch_ppp(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int M, int N, int K, const Epi& ep,
-               hipStream_t s) {
-  static bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)gemm_ppp_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              PP_LDS_MAX);
-    return true;
-  }();
-  (void)attr;
+inline int cu_count() {
   static int cus = [] {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
     return n;
   }();
-  const int lds = ppp_lds_bytes(EPI, N, ep);
+  return cus;
+}
+
+// Row tile of the persistent form: 256, or 192 when whole rounds of 192-row
+// tiles over the CUs cost at least 10% less (the N = 1024 projections at
+// M = 21,984: 344 tiles = 1.34 rounds at 256 rows, 460 = 1.80 at 192); the
+// residual epilogue always uses 192 rows (register budget: rx + acc)
+inline int ppp_pick_bm(int epi, int M, int N) {
+  if (epi == VGGT_EPI_RESID_F32) return 192;
+  static int force = [] {  // VGGT_GEMM_BM=192/256: A/B override
+    const char* e = getenv("VGGT_GEMM_BM");
+    return e ? atoi(e) : 0;
+  }();
+  if (force == 192 || force == 256) return force;
+  const int cus = cu_count();
+  const long r256 = ((long)((M + 255) / 256) * (N / 256) + cus - 1) / cus;
+  const long r192 = ((long)((M + 191) / 192) * (N / 256) + cus - 1) / cus;
+  return r192 * 192 * 10 < r256 * 256 * 9 ? 192 : 256;
+}
+
+template <int EPI, int BMT>
+int launch_ppp_bm(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int M, int N, int K, const Epi& ep,
+                  hipStream_t s) {
+  static bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)gemm_ppp_kernel<EPI, BMT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              PP_LDS_MAX);
+    return true;
+  }();
+  (void)attr;
+  const int lds = ppp_lds_bytes(EPI, BMT, N, ep);
   if (!lds) return VGGT_ERR_SHAPE;
-  const int ntiles = ((M + PBM - 1) / PBM) * (N / 256);
-  const int nwg = ntiles < cus ? ntiles : cus;
-  gemm_ppp_kernel<EPI><<<nwg, PNT, lds, s>>>(a, lda, w, ldw, M, N, K, ep);
+  const int ntiles = ((M + BMT - 1) / BMT) * (N / 256);
+  const int nwg = ntiles < cu_count() ? ntiles : cu_count();
+  gemm_ppp_kernel<EPI, BMT><<<nwg, PNT, lds, s>>>(a, lda, w, ldw, M, N, K, ep);
   return VGGT_OK;
+}
+
+template <int EPI>
+int launch_ppp(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int M, int N, int K, const Epi& ep,
+               hipStream_t s) {
+  if constexpr (EPI == VGGT_EPI_RESID_F32) {
+    return launch_ppp_bm<EPI, 192>(a, lda, w, ldw, M, N, K, ep, s);
+  } else {
+    if (ppp_pick_bm(EPI, M, N) == 192) return launch_ppp_bm<EPI, 192>(a, lda, w, ldw, M, N, K, ep, s);
+    return launch_ppp_bm<EPI, 256>(a, lda, w, ldw, M, N, K, ep, s);
+  }
 }
 
 // Ping-pong tile width for an N-wide output: the BN whose whole rounds of
@@ -1394,21 +1486,30 @@ int gemm_impl(const void* A, int64_t lda, const void* W, int64_t ldw, const floa
   // shape 159 -> 139 us, scripts/gemmbench.py r3i); it falls back to mode 7
   // for the epilogues it does not cover
   if (g_vggt_gemm_tile < 0 && mode == 7 && M >= 16384 && N <= PP_MAXN && (persist_policy() & 1)) mode = 9;
+  // the LayerScale-residual fc2 (N = 1024, K = 4096) on 192-row persistent tiles:
+  // 216 -> 201 us, aggregator step 104.0 -> 102.3 ms (same box, r3o); the
+  // K = 1024 proj stays on the 128x128 form (76 vs 80 us)
+  if (g_vggt_gemm_tile < 0 && epi == VGGT_EPI_RESID_F32 && M >= 16384 && N % 256 == 0 && N <= PP_MAXN &&
+      K % PBK == 0 && K >= 2048 && (persist_policy() & 4))
+    mode = 9;
   if (mode >= 3 && mode <= 7 && K % PBK) mode = 2;    // the ping-pong form steps K by 64
   if (mode == 0 && K % BK) mode = 2;     // the 128x128 form steps K by 64
   if (mode == 1 && N % 256) mode = 2;
   // per-lane 32-bit DMA offsets span one 256-row panel
   if (mode != 0 && (int64_t)RBM * (lda > ldw ? lda : ldw) * 2 >= (1ll << 31)) return VGGT_ERR_SHAPE;
-  if (mode == 9 && (N % 256 || N > PP_MAXN || K % PBK || epi == VGGT_EPI_RESID_F32 || out2 ||
-                    (int64_t)PBM * (ldo > 0 ? ldo : 1) * 4 >= (1ll << 31)))
-    mode = K % PBK ? 2 : 7;  // the persistent form covers the bf16 / GELU / f32 epilogues up to N = 4096
+  if (mode == 9 && (N % 256 || N > PP_MAXN || K % PBK || (epi == VGGT_EPI_GELU_BF16 && out2) ||
+                    (int64_t)PBM * (ldo > ldo2 ? ldo : ldo2) * 4 >= (1ll << 31)))
+    mode = K % PBK ? 2 : epi == VGGT_EPI_RESID_F32 ? 0 : 7;  // the persistent form: N % 256 == 0, N <= 4096
   if (mode == 9) {
+    int rc;
     switch (epi) {
-      case VGGT_EPI_BF16: launch_ppp<VGGT_EPI_BF16>(a, lda, w, ldw, M, N, K, ep, s); break;
-      case VGGT_EPI_GELU_BF16: launch_ppp<VGGT_EPI_GELU_BF16>(a, lda, w, ldw, M, N, K, ep, s); break;
-      case VGGT_EPI_F32: launch_ppp<VGGT_EPI_F32>(a, lda, w, ldw, M, N, K, ep, s); break;
+      case VGGT_EPI_BF16: rc = launch_ppp<VGGT_EPI_BF16>(a, lda, w, ldw, M, N, K, ep, s); break;
+      case VGGT_EPI_GELU_BF16: rc = launch_ppp<VGGT_EPI_GELU_BF16>(a, lda, w, ldw, M, N, K, ep, s); break;
+      case VGGT_EPI_RESID_F32: rc = launch_ppp<VGGT_EPI_RESID_F32>(a, lda, w, ldw, M, N, K, ep, s); break;
+      case VGGT_EPI_F32: rc = launch_ppp<VGGT_EPI_F32>(a, lda, w, ldw, M, N, K, ep, s); break;
       default: return VGGT_ERR_UNSUPPORTED;
     }
+    if (rc != VGGT_OK) return rc;
     HIP_LAUNCH_CHECK();
     return VGGT_OK;
   }
@@ -1519,7 +1620,7 @@ extern "C" int vggt_gemm_qkv(const void* A, int64_t lda, const void* W, int64_t 
   if (g_vggt_gemm_tile < 0 && mode == 7 && M >= 16384 && (persist_policy() & 2)) mode = 9;
   if (mode == 9) {
     bool ok = D == 64 && N % 256 == 0 && N <= PP_MAXN && K % PBK == 0 && rope_mode != VGGT_ROPE_1D &&
-              (int64_t)PBM * ldo * 2 < (1ll << 31) && ppp_lds_bytes(EPI_QKNORM_D64, N, ep) > 0;
+              (int64_t)PBM * ldo * 2 < (1ll << 31) && ppp_lds_bytes(EPI_QKNORM_D64, ppp_pick_bm(EPI_QKNORM_D64, M, N), N, ep) > 0;
     if (ok && rope_mode == VGGT_ROPE_2D) {
       // positions are staged as bytes; tables of at most 256 positions
       ok = tab_len <= 256;
