@@ -20,6 +20,7 @@
 
 #include "common.h"
 #include "tune.h"
+#include "gelu_lut.h"
 
 namespace {
 
@@ -970,6 +971,29 @@ int launch_pp(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int M,
 // ===========================================================================
 constexpr int PP_MAXN = 4096;
 constexpr int PP_LDS_MAX = 160 * 1024;
+
+// bf16 GELU of the two bf16 values packed in d, from the LDS copy of
+// gelu_lut (|x| in [2^-16, 2^6): positive half, then negative half).  Outside
+// the table (rare: a wave-uniform branch) the limits of torch's float32
+// formula: bf16(0.5 x) below it, x or -0.0 above it (scripts/gen_gelu_lut.py
+// checks both rules against torch for every bf16 value).
+__device__ __forceinline__ uint32_t gelu1_lut(uint32_t b, const uint16_t* lut) {
+  const uint32_t u = b & 0x7fff;
+  const uint32_t t = u - (GELU_LUT_E0 << 7);
+  if (t < (uint32_t)GELU_LUT_N) return lut[t + ((b >> 15) & 1) * GELU_LUT_N];
+  if (u < (GELU_LUT_E0 << 7)) return f2bf(0.5f * bf2f((bf16_t)b));
+  return (b & 0x8000) ? 0x8000u : b;
+}
+__device__ __forceinline__ uint32_t gelu2_lut(uint32_t d, const uint16_t* lut) {
+  const uint32_t tlo = (d & 0x7fff) - (GELU_LUT_E0 << 7);
+  const uint32_t thi = ((d >> 16) & 0x7fff) - (GELU_LUT_E0 << 7);
+  if (__builtin_amdgcn_ballot_w64(max(tlo, thi) >= (uint32_t)GELU_LUT_N) == 0) {
+    const uint32_t lo = lut[tlo + ((d >> 15) & 1) * GELU_LUT_N];
+    const uint32_t hi = lut[thi + (d >> 31) * GELU_LUT_N];
+    return lo | (hi << 16);
+  }
+  return gelu1_lut(d & 0xffff, lut) | (gelu1_lut(d >> 16, lut) << 16);
+}
 // VGGT_GEMM_PERSIST (A/B of the auto policy): bit 0 = the persistent form for
 // the bf16 / GELU / f32 GEMMs, bit 1 = for the fused qkv GEMM, bit 2 = for the
 // LayerScale-residual GEMMs (default all)
@@ -1029,6 +1053,9 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
   float* gam_s = bias_s + N;  // RESID: LayerScale gamma
   if constexpr (EPI == VGGT_EPI_RESID_F32)
     for (int i = threadIdx.x; i < N; i += PNT) gam_s[i] = ep.gamma[i];
+  uint16_t* lut_s = (uint16_t*)(bias_s + N);  // GELU: the bf16 table
+  if constexpr (EPI == VGGT_EPI_GELU_BF16)
+    for (int i = threadIdx.x; i < GELU_LUT_N; i += PNT) ((uint32_t*)lut_s)[i] = ((const uint32_t*)gelu_lut)[i];
   // EPI_QKNORM_D64: q/k norm weights (qw qb kw kb, 64 each), RoPE-2D cos / sin
   // tables [tab_len][32] and the positions (y | x << 8 per position index)
   float* qkn_s = bias_s + N;
@@ -1312,18 +1339,17 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
 #pragma unroll
         for (int mi = 0; mi < C::MI; ++mi) {
           const int ml = wm * C::HM + mi * 16 + (lane & 15);
-          f32x4 v0 = acc[np][mi] + bv0, v1 = acc[np + 1][mi] + bv1;
-          if constexpr (EPI == VGGT_EPI_GELU_BF16) {
-            // GELU of the bf16-rounded Linear output (autocast), rounded to bf16
-            const f32x2 g0 = gelu_fast2(f32x2{round_bf(v0[0]), round_bf(v0[1])});
-            const f32x2 g1 = gelu_fast2(f32x2{round_bf(v0[2]), round_bf(v0[3])});
-            const f32x2 g2 = gelu_fast2(f32x2{round_bf(v1[0]), round_bf(v1[1])});
-            const f32x2 g3 = gelu_fast2(f32x2{round_bf(v1[2]), round_bf(v1[3])});
-            v0 = f32x4{g0[0], g0[1], g1[0], g1[1]};
-            v1 = f32x4{g2[0], g2[1], g3[0], g3[1]};
-          }
+          const f32x4 v0 = acc[np][mi] + bv0, v1 = acc[np + 1][mi] + bv1;
           uint32_t a0 = pack_bf2(v0[0], v0[1]), a1 = pack_bf2(v0[2], v0[3]);
           uint32_t b0 = pack_bf2(v1[0], v1[1]), b1 = pack_bf2(v1[2], v1[3]);
+          if constexpr (EPI == VGGT_EPI_GELU_BF16) {
+            // GELU of the bf16 Linear output (autocast), from the LDS table of
+            // torch's float32 GELU rounded to bf16 (gelu_lut.h)
+            a0 = gelu2_lut(a0, lut_s);
+            a1 = gelu2_lut(a1, lut_s);
+            b0 = gelu2_lut(b0, lut_s);
+            b1 = gelu2_lut(b1, lut_s);
+          }
           // rows 1 <-> 0 and 3 <-> 2 of (a = fragment np, b = fragment np+1)
           const auto s0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
           const auto s1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
@@ -1349,6 +1375,7 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
 inline int ppp_lds_bytes(int epi, int bmt, int N, const Epi& ep) {
   int64_t b = 2 * ((int64_t)bmt * PBK * 2 + 256 * PBK * 2) + (int64_t)N * 4;
   if (epi == VGGT_EPI_RESID_F32) b += (int64_t)N * 4;
+  if (epi == VGGT_EPI_GELU_BF16) b += (int64_t)GELU_LUT_N * 2 * 2;
   if (epi == EPI_QKNORM_D64) {
     b += 256 * 4;
     if (ep.rope_mode == VGGT_ROPE_2D) b += 2 * (int64_t)ep.tab_len * 32 * 4 + (((int64_t)ep.period * 2 + 15) & ~15);
@@ -1403,6 +1430,8 @@ template <int EPI>
 int launch_ppp(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int M, int N, int K, const Epi& ep,
                hipStream_t s) {
   if constexpr (EPI == VGGT_EPI_RESID_F32) {
+    // (128-row residual tiles measured slower: proj 81.7 vs 67.4 us on the
+    // 128x128 form, aggregator step 104.9 vs 101.3 ms, r3r)
     return launch_ppp_bm<EPI, 192>(a, lda, w, ldw, M, N, K, ep, s);
   } else {
     if (ppp_pick_bm(EPI, M, N) == 192) return launch_ppp_bm<EPI, 192>(a, lda, w, ldw, M, N, K, ep, s);

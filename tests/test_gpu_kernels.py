@@ -462,3 +462,26 @@ def _qkv_fused_check(N, tile, D, H, mode, norm, M, K):
     # identical arithmetic up to fp32 contraction order: at most one bf16 ulp apart
     assert (d <= ref.float().abs() * 2 ** -7 + 1e-6).all(), d.max().item()
     assert torch.equal(out[:, 2 * C:], ref[:, 2 * C:])  # v block untouched
+
+
+@pytest.mark.parametrize("scale", [1.0, 40.0, 1e-6])
+def test_gemm_gelu_lut_exact(N, scale):
+    """Persistent-form fc1 epilogue (mode 9): GELU from the LDS table of torch's
+    float32 GELU is bit-exact against torch (CPU) applied to the same bf16
+    Linear output -- including pre-activations outside the table (|x| < 2^-16
+    and |x| >= 64, the scale 1e-6 / 40 cases) that take the limit rules."""
+    prev = N.tune(N.TUNE_GEMM_TILE, 9)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(5)
+        M, K, Nn = 4100, 1024, 1024
+        a = (torch.randn(M, K, device="cuda", generator=g) * scale).to(torch.bfloat16)
+        w = (torch.randn(Nn, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
+        b = torch.zeros(Nn, device="cuda")
+        pre = torch.empty(M, Nn, device="cuda", dtype=torch.bfloat16)
+        out = torch.empty_like(pre)
+        N.gemm_bf16(a, w, b, pre, N.EPI_BF16)
+        N.gemm_bf16(a, w, b, out, N.EPI_GELU_BF16)
+        ref = F.gelu(pre.float().cpu()).to(torch.bfloat16)
+        assert torch.equal(out.cpu().view(torch.int16), ref.view(torch.int16))
+    finally:
+        N.tune(N.TUNE_GEMM_TILE, prev)
