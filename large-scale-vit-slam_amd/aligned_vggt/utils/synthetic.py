@@ -3,8 +3,11 @@ configs use random-init weights and synthetic frames; no checkpoint or dataset
 is available offline -- SURVEY.md §8d).
 
 Every parameter draws from its own CPU ``torch.Generator`` seeded by
-``crc32(name) ^ seed``, so a module tree gets identical weights on any device
-and in any construction order.
+``crc32(name) ^ seed``, so a module tree gets identical weights on any device,
+in any construction order and in every process (parameters with a specific
+reference init -- tiny-std tokens, the orthonormal memory tokens, the gate
+weight -- are redrawn from their reference distribution; constant inits are
+kept).
 """
 from __future__ import annotations
 
@@ -13,9 +16,13 @@ import zlib
 import torch
 import torch.nn as nn
 
-# parameters whose constructor init is the reference's and is kept as is
-_KEEP = ("gamma", "camera_token", "register_token", "register_tokens", "cls_token", "mask_token",
-         "per_frame_alignment_token", "memory_token", "alpha", "empty_pose_tokens", "gate_mlp.2.")
+# parameters whose constructor init is the reference's distribution, redrawn
+# from the per-name generator with that same distribution (the constructors
+# draw from torch's global generator, whose seed differs per process)
+_REF_NORMAL = {"camera_token": 1e-6, "register_token": 1e-6, "register_tokens": 1e-6, "cls_token": 1e-6,
+               "per_frame_alignment_token": 1e-6, "gate_mlp.2.weight": 0.1}
+# constant constructor inits, kept as is
+_KEEP = ("gamma", "mask_token", "alpha", "empty_pose_tokens", "gate_mlp.2.bias")
 
 
 @torch.no_grad()
@@ -24,6 +31,17 @@ def synthetic_init_(model: nn.Module, seed: int = 0, std: float = 0.02) -> nn.Mo
         if any(k in name for k in _KEEP):
             continue
         g = torch.Generator().manual_seed((zlib.crc32(name.encode()) ^ seed) & 0x7FFFFFFF)
+        leaf = name.split(".")[-1]
+        ref_std = _REF_NORMAL.get(leaf, _REF_NORMAL.get(".".join(name.split(".")[-3:])))
+        if ref_std is not None:
+            p.copy_((ref_std * torch.randn(p.shape, generator=g)).to(p.device, p.dtype))
+            continue
+        if leaf == "memory_token":
+            # alignment_head.py:211-214: orthonormal rows, then L2-normalised
+            m = torch.empty(p.shape[1:], dtype=torch.float32)
+            nn.init.orthogonal_(m, generator=g)
+            p.copy_(torch.nn.functional.normalize(m, dim=-1).view(p.shape).to(p.device, p.dtype))
+            continue
         r = torch.randn(p.shape, generator=g, dtype=torch.float32)
         is_norm_w = p.dim() == 1 and name.endswith("weight") and "norm" in name.split(".")[-2]
         if is_norm_w:

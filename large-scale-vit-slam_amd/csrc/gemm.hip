@@ -1514,7 +1514,11 @@ int gemm_impl(const void* A, int64_t lda, const void* W, int64_t ldw, const floa
   // rounds of CUs (the 16x518^2 chunk: fc1 + GELU 217 -> 204 us, plain qkv
   // shape 159 -> 139 us, scripts/gemmbench.py r3i); it falls back to mode 7
   // for the epilogues it does not cover
-  if (g_vggt_gemm_tile < 0 && mode == 7 && M >= 16384 && N <= PP_MAXN && (persist_policy() & 1)) mode = 9;
+  // (GELU from M = 4,096: the 154x518 sequence chunk's fc1, 6,592 rows: 72.9 -> 64.8 us, r3w; plain bf16 stays on
+  // the one-shot forms below 16,384 rows: qkv shape 49-55 vs 55 us)
+  if (g_vggt_gemm_tile < 0 && mode == 7 && (M >= 16384 || epi == VGGT_EPI_GELU_BF16) && N <= PP_MAXN &&
+      (persist_policy() & 1))
+    mode = 9;
   // the LayerScale-residual fc2 (N = 1024, K = 4096) on 192-row persistent tiles:
   // 216 -> 201 us, aggregator step 104.0 -> 102.3 ms (same box, r3o); the
   // K = 1024 proj stays on the 128x128 form (76 vs 80 us)
@@ -1646,7 +1650,8 @@ extern "C" int vggt_gemm_qkv(const void* A, int64_t lda, const void* W, int64_t 
   if (mode == 1 && hd % 256) mode = 2;
   if (mode != 0 && (int64_t)RBM * (lda > ldw ? lda : ldw) * 2 >= (1ll << 31)) return VGGT_ERR_SHAPE;
   // auto: the persistent form on the chunk shapes (D = 64 heads, RoPE-2D or none)
-  if (g_vggt_gemm_tile < 0 && mode == 7 && M >= 16384 && (persist_policy() & 2)) mode = 9;
+  // (fused qkv of the 154x518 sequence chunk, 6,592 rows: 68.9 -> 53.6 us, r3w)
+  if (g_vggt_gemm_tile < 0 && mode == 7 && M >= 4096 && (persist_policy() & 2)) mode = 9;
   if (mode == 9) {
     bool ok = D == 64 && N % 256 == 0 && N <= PP_MAXN && K % PBK == 0 && rope_mode != VGGT_ROPE_1D &&
               (int64_t)PBM * ldo * 2 < (1ll << 31) && ppp_lds_bytes(EPI_QKNORM_D64, ppp_pick_bm(EPI_QKNORM_D64, M, N), N, ep) > 0;
