@@ -48,6 +48,33 @@ struct Epi {
 
 constexpr int EPI_QKNORM_D64 = 16, EPI_QKNORM_D128 = 17;  // internal epilogue ids
 
+// bf16 GELU of the two bf16 values packed in d, from gelu_lut (global memory)
+// or its LDS copy (|x| in [2^-16, 2^6): positive half, then negative half).  Outside
+// the table (rare: a wave-uniform branch) the limits of torch's float32
+// formula: bf16(0.5 x) below it, x or -0.0 above it (scripts/gen_gelu_lut.py
+// checks both rules against torch for every bf16 value).
+template <typename TP>
+__device__ __forceinline__ uint32_t gelu1_lut(uint32_t b, TP lut) {
+  const uint32_t u = b & 0x7fff;
+  const uint32_t t = u - (GELU_LUT_E0 << 7);
+  if (t < (uint32_t)GELU_LUT_N) return lut[t + ((b >> 15) & 1) * GELU_LUT_N];
+  if (u < (GELU_LUT_E0 << 7)) return f2bf(0.5f * bf2f((bf16_t)b));
+  return (b & 0x8000) ? 0x8000u : b;
+}
+template <typename TP>
+__device__ __forceinline__ uint32_t gelu2_lut(uint32_t d, TP lut) {
+  const uint32_t tlo = (d & 0x7fff) - (GELU_LUT_E0 << 7);
+  const uint32_t thi = ((d >> 16) & 0x7fff) - (GELU_LUT_E0 << 7);
+  if (__builtin_amdgcn_ballot_w64(max(tlo, thi) >= (uint32_t)GELU_LUT_N) == 0) {
+    const uint32_t lo = lut[tlo + ((d >> 15) & 1) * GELU_LUT_N];
+    const uint32_t hi = lut[thi + (d >> 31) * GELU_LUT_N];
+    return lo | (hi << 16);
+  }
+  return gelu1_lut(d & 0xffff, lut) | (gelu1_lut(d >> 16, lut) << 16);
+}
+// the global-memory table (the LDS-staged epilogues of the one-shot forms)
+__device__ __forceinline__ uint32_t gelu2_tab(uint32_t d, const uint16_t* lut) { return gelu2_lut(d, lut); }
+
 // ---- epilogue 2 (shared): the bf16 C tile staged in LDS (row stride CROW
 // bytes) re-read as whole rows, 16 B (8 features) per thread, and written with
 // coalesced stores, applying GELU / LayerScale + fp32 residual there.
@@ -175,13 +202,14 @@ __device__ __forceinline__ void write_tile(const char* Cs, int m0, int n0, int M
       if constexpr (EPI == VGGT_EPI_GELU_BF16) {
         // the pre-activation (bf16 Linear output) for the GELU backward
         if (ep.out2) *(uint4*)((bf16_t*)(void*)ep.out2 + (int64_t)m * ep.ldo2 + n) = cv;
+        // GELU of the bf16 Linear output from the table of torch's float32
+        // GELU (the persistent form reads the same table from LDS): every
+        // GEMM form gives bit-identical activations
         uint4 o;
-        const f32x2 g0 = gelu_fast2(f32x2{v[0], v[1]}), g1 = gelu_fast2(f32x2{v[2], v[3]});
-        const f32x2 g2 = gelu_fast2(f32x2{v[4], v[5]}), g3 = gelu_fast2(f32x2{v[6], v[7]});
-        o.x = pack_bf2(g0[0], g0[1]);
-        o.y = pack_bf2(g1[0], g1[1]);
-        o.z = pack_bf2(g2[0], g2[1]);
-        o.w = pack_bf2(g3[0], g3[1]);
+        o.x = gelu2_tab(cv.x, gelu_lut);
+        o.y = gelu2_tab(cv.y, gelu_lut);
+        o.z = gelu2_tab(cv.z, gelu_lut);
+        o.w = gelu2_tab(cv.w, gelu_lut);
         *(uint4*)((bf16_t*)ep.out + (int64_t)m * ep.ldo + n) = o;
       } else if constexpr (EPI == VGGT_EPI_RESID_F32) {
         float* xp = (float*)ep.out + (int64_t)m * ep.ldo + n;
@@ -972,28 +1000,6 @@ int launch_pp(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int M,
 constexpr int PP_MAXN = 4096;
 constexpr int PP_LDS_MAX = 160 * 1024;
 
-// bf16 GELU of the two bf16 values packed in d, from the LDS copy of
-// gelu_lut (|x| in [2^-16, 2^6): positive half, then negative half).  Outside
-// the table (rare: a wave-uniform branch) the limits of torch's float32
-// formula: bf16(0.5 x) below it, x or -0.0 above it (scripts/gen_gelu_lut.py
-// checks both rules against torch for every bf16 value).
-__device__ __forceinline__ uint32_t gelu1_lut(uint32_t b, const uint16_t* lut) {
-  const uint32_t u = b & 0x7fff;
-  const uint32_t t = u - (GELU_LUT_E0 << 7);
-  if (t < (uint32_t)GELU_LUT_N) return lut[t + ((b >> 15) & 1) * GELU_LUT_N];
-  if (u < (GELU_LUT_E0 << 7)) return f2bf(0.5f * bf2f((bf16_t)b));
-  return (b & 0x8000) ? 0x8000u : b;
-}
-__device__ __forceinline__ uint32_t gelu2_lut(uint32_t d, const uint16_t* lut) {
-  const uint32_t tlo = (d & 0x7fff) - (GELU_LUT_E0 << 7);
-  const uint32_t thi = ((d >> 16) & 0x7fff) - (GELU_LUT_E0 << 7);
-  if (__builtin_amdgcn_ballot_w64(max(tlo, thi) >= (uint32_t)GELU_LUT_N) == 0) {
-    const uint32_t lo = lut[tlo + ((d >> 15) & 1) * GELU_LUT_N];
-    const uint32_t hi = lut[thi + (d >> 31) * GELU_LUT_N];
-    return lo | (hi << 16);
-  }
-  return gelu1_lut(d & 0xffff, lut) | (gelu1_lut(d >> 16, lut) << 16);
-}
 // VGGT_GEMM_PERSIST (A/B of the auto policy): bit 0 = the persistent form for
 // the bf16 / GELU / f32 GEMMs, bit 1 = for the fused qkv GEMM, bit 2 = for the
 // LayerScale-residual GEMMs (default all)

@@ -464,13 +464,15 @@ def _qkv_fused_check(N, tile, D, H, mode, norm, M, K):
     assert torch.equal(out[:, 2 * C:], ref[:, 2 * C:])  # v block untouched
 
 
+@pytest.mark.parametrize("tile", [0, 4, 8, 9])
 @pytest.mark.parametrize("scale", [1.0, 40.0, 1e-6])
-def test_gemm_gelu_lut_exact(N, scale):
-    """Persistent-form fc1 epilogue (mode 9): GELU from the LDS table of torch's
-    float32 GELU is bit-exact against torch (CPU) applied to the same bf16
-    Linear output -- including pre-activations outside the table (|x| < 2^-16
-    and |x| >= 64, the scale 1e-6 / 40 cases) that take the limit rules."""
-    prev = N.tune(N.TUNE_GEMM_TILE, 9)
+def test_gemm_gelu_lut_exact(N, scale, tile):
+    """fc1 epilogue of every GEMM form: GELU from the table of torch's float32
+    GELU (LDS copy in the persistent form, global memory in the others) is
+    bit-exact against torch (CPU) applied to the same bf16 Linear output --
+    including pre-activations outside the table (|x| < 2^-16 and |x| >= 64,
+    the scale 1e-6 / 40 cases) that take the limit rules."""
+    prev = N.tune(N.TUNE_GEMM_TILE, tile)
     try:
         g = torch.Generator(device="cuda").manual_seed(5)
         M, K, Nn = 4100, 1024, 1024
