@@ -1031,10 +1031,27 @@ struct PPXCfg {
   static constexpr int WL = WBYTES / 1024 / 8;
 };
 
+// Tile t -> (M-tile, N-tile), grouped by gm M-tiles (gm <= 1: row-major).  An
+// XCD's concurrent tiles are consecutive t, so with gm = 4 and 32 CUs per XCD a
+// round covers 4 M-panels x 8 N-panels instead of 2 x 16 (fc1): 12 instead of 18
+// distinct K-slices per K-step fetched into that XCD's L2.
+__device__ __forceinline__ void grouped_tile(int t, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
+  if (gm <= 1) {
+    tm = t / tiles_n;
+    tn = t - tm * tiles_n;
+    return;
+  }
+  const int per = gm * tiles_n;
+  const int g = t / per, r = t - g * per;
+  const int rows = min(gm, tiles_m - g * gm);
+  tm = g * gm + r % rows;
+  tn = r / rows;
+}
+
 template <int EPI, int BMT>
 __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                           const bf16_t* __restrict__ W, int64_t ldw, int M, int N,
-                                                          int K, Epi ep) {
+                                                          int K, Epi ep, int gm) {
   constexpr int BN = 256;
   using C = PPXCfg<BMT>;
   static_assert(C::AL * 1024 * 8 == C::ABYTES, "whole DMA pieces per wave");
@@ -1101,8 +1118,9 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
   int32x4 ra, rw;
   uint32_t aoff[C::AL], woff[C::WL];
   auto setup = [&](int tile) {
-    const int t = xcd_remap(tile, ntiles);
-    const int m0 = (t / tiles_n) * BMT, n0 = (t % tiles_n) * BN;
+    int tm, tn;
+    grouped_tile(xcd_remap(tile, ntiles), tiles_m, tiles_n, gm, tm, tn);
+    const int m0 = tm * BMT, n0 = tn * BN;
     ra = make_rsrc_u(A + (int64_t)m0 * lda);
     rw = make_rsrc_u(W + (int64_t)n0 * ldw);
 #pragma unroll
@@ -1159,8 +1177,9 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
   }
   bool stores_out = false;  // this wave has NST epilogue stores younger than K-tile 1's DMA
   for (;;) {
-    const int t = xcd_remap(tile, ntiles);
-    const int m0 = (t / tiles_n) * BMT, n0 = (t % tiles_n) * BN;
+    int tm, tn;
+    grouped_tile(xcd_remap(tile, ntiles), tiles_m, tiles_n, gm, tm, tn);
+    const int m0 = tm * BMT, n0 = tn * BN;
 #pragma unroll
     for (int i = 0; i < C::NI; ++i)
 #pragma unroll
@@ -1428,7 +1447,14 @@ int launch_ppp_bm(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, in
   if (!lds) return VGGT_ERR_SHAPE;
   const int ntiles = ((M + BMT - 1) / BMT) * (N / 256);
   const int nwg = ntiles < cu_count() ? ntiles : cu_count();
-  gemm_ppp_kernel<EPI, BMT><<<nwg, PNT, lds, s>>>(a, lda, w, ldw, M, N, K, ep);
+  // M-tiles per tile group (VGGT_GEMM_GM overrides; 0 = row-major).  Aggregator
+  // step 98.45 -> 97.3-97.6 ms at 4 (8: 97.55, 16: 98.5); fc1 at K = 4096 625 ->
+  // 591 us (r3y, r3z)
+  static int gm = [] {
+    const char* e = getenv("VGGT_GEMM_GM");
+    return e ? atoi(e) : 4;
+  }();
+  gemm_ppp_kernel<EPI, BMT><<<nwg, PNT, lds, s>>>(a, lda, w, ldw, M, N, K, ep, gm);
   return VGGT_OK;
 }
 

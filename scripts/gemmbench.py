@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--tokens", type=int, default=16 * 1374)
     ap.add_argument("--warm-s", type=float, default=3.0)
     ap.add_argument("--shapes", default="qkv,proj,fc1,fc2,fc1_k4096")
+    ap.add_argument("--epis", default="torch,plain,gelu,resid")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
@@ -61,15 +62,18 @@ def main():
         bias = torch.randn(Nn, device=dev) * 0.1
         fl = 2.0 * M * Nn * K
         ob = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
-        us = timeit(lambda: torch.matmul(a, w.t(), out=ob), args.reps)
-        res[f"{name}/torch"] = {"us": round(us, 1), "tflops": round(fl / us / 1e6, 1)}
-        print(f"{name}/torch", res[f"{name}/torch"], flush=True)
+        if "torch" in args.epis.split(","):
+            us = timeit(lambda: torch.matmul(a, w.t(), out=ob), args.reps)
+            res[f"{name}/torch"] = {"us": round(us, 1), "tflops": round(fl / us / 1e6, 1)}
+            print(f"{name}/torch", res[f"{name}/torch"], flush=True)
         xr = torch.randn(M, Nn, device=dev)
         gamma = torch.rand(Nn, device=dev)
         for mode in map(int, args.modes.split(",")):
             prev = N.tune(N.TUNE_GEMM_TILE, mode)
             try:
                 for epi, en in ((N.EPI_BF16, "plain"), (N.EPI_GELU_BF16, "gelu"), (N.EPI_RESID_F32, "resid")):
+                    if en not in args.epis.split(","):
+                        continue
                     if epi == N.EPI_RESID_F32:
                         fn = lambda: N.gemm_bf16(a, w, bias, xr, epi, gamma=gamma)  # noqa: E731
                     else:
