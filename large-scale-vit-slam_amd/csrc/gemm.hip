@@ -1048,10 +1048,10 @@ __device__ __forceinline__ void grouped_tile(int t, int tiles_m, int tiles_n, in
   tn = r / rows;
 }
 
-template <int EPI, int BMT>
+template <int EPI, int BMT, bool FK>
 __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                           const bf16_t* __restrict__ W, int64_t ldw, int M, int N,
-                                                          int K, Epi ep, int gm) {
+                                                          int K, Epi ep, int sched) {
   constexpr int BN = 256;
   using C = PPXCfg<BMT>;
   static_assert(C::AL * 1024 * 8 == C::ABYTES, "whole DMA pieces per wave");
@@ -1071,6 +1071,8 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
   const int ntiles = tiles_m * tiles_n;
   const int nk = K / PBK;
   const int wm = wave >> 2, wn = wave & 3;
+  const bool split = (sched >> 8) & 1;
+  const int gm = sched & 255;
 
   for (int i = threadIdx.x; i < N; i += PNT) bias_s[i] = ep.bias[i];
   float* gam_s = bias_s + N;  // RESID: LayerScale gamma
@@ -1143,6 +1145,22 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
 #pragma unroll
     for (int i = 0; i < C::WL; ++i) dma16s(rw, woff[i], soff, b + C::ABYTES + (wave * C::WL + i) * 1024);
   };
+  // split staging (sched bit 8, default; VGGT_GEMM_SPLITDMA=0 turns it off): the W
+  // pieces at READ(kt, 0), the A pieces at READ(kt, 1), so both READ segments carry
+  // half of the K-tile's DMA instead of one carrying all of it next to its 12
+  // ds_reads (gemmbench r3v: fc1 at K = 4096 597.6 -> 569.6 us, plain qkv 146 -> 140 us)
+  auto stage_w = [&](int buf, int kt) {
+    const uint32_t b = lds0 + buf * C::BUF;
+    const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(kt * PBK * 2));
+#pragma unroll
+    for (int i = 0; i < C::WL; ++i) dma16s(rw, woff[i], soff, b + C::ABYTES + (wave * C::WL + i) * 1024);
+  };
+  auto stage_a = [&](int buf, int kt) {
+    const uint32_t b = lds0 + buf * C::BUF;
+    const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(kt * PBK * 2));
+#pragma unroll
+    for (int i = 0; i < C::AL; ++i) dma16s(ra, aoff[i], soff, b + (wave * C::AL + i) * 1024);
+  };
 
   f32x4 acc[C::NI][C::MI];
   bf16x8 af[C::MI], wf[C::NI];
@@ -1160,6 +1178,29 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
 #pragma unroll
       for (int ni = 0; ni < C::NI; ++ni)
         acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], af[mi], acc[ni][mi], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // FK: one READ / MATH segment per whole K-tile (both K halves' fragments held)
+  bf16x8 af2[FK ? C::MI : 1], wf2[FK ? C::NI : 1];
+  auto read_frags2 = [&](int buf) {
+    const char* base = smem + buf * C::BUF;
+#pragma unroll
+    for (int i = 0; i < C::NI; ++i) wf2[i] = *(const bf16x8*)(base + w_off[1] + i * 16 * 128);
+#pragma unroll
+    for (int i = 0; i < C::MI; ++i) af2[i] = *(const bf16x8*)(base + a_off[1] + i * 16 * 128);
+  };
+  auto math2 = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mi = 0; mi < C::MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < C::NI; ++ni)
+        acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], af[mi], acc[ni][mi], 0, 0, 0);
+#pragma unroll
+    for (int mi = 0; mi < C::MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < C::NI; ++ni)
+        acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf2[ni], af2[mi], acc[ni][mi], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -1185,24 +1226,61 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
 #pragma unroll
       for (int j = 0; j < C::MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (wm == 1) asm volatile("s_barrier" ::: "memory");  // stagger the second M half by one segment
+    if constexpr (FK) {
+      for (int kt = 0; kt < nk; ++kt) {
+        const int buf = (b0 + kt) & 1;
+        const bool pf = kt >= 1 && kt + 1 < nk;
+        // READ(kt): K-tile kt+1's W pieces, then its A pieces; both K halves' fragments.
+        // The W pieces (read by both wave halves from the next segment on) land
+        // before this segment's barrier, the A pieces (read by this half two
+        // segments later) before the MATH segment's.
+        if (pf) {
+          stage_w(buf ^ 1, kt + 1);
+          stage_a(buf ^ 1, kt + 1);
+        }
+        read_frags(buf, 0);
+        read_frags2(buf);
+        if (pf) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::AL) : "memory");
+        else if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NST) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        math2();
+        __builtin_amdgcn_sched_barrier(0);
+        if (pf) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_barrier" ::: "memory");
+      }
+    } else
     for (int kt = 0; kt < nk; ++kt) {
       const int buf = (b0 + kt) & 1;
-      // READ(kt, 0): K-tile kt+1's DMA (K-tile 1 was issued ahead), this step's fragments
-      if (kt >= 1 && kt + 1 < nk) stage(buf ^ 1, kt + 1);
+      const bool pf = kt >= 1 && kt + 1 < nk;  // this step issues K-tile kt+1 (K-tile 1 was issued ahead)
+      // READ(kt, 0): K-tile kt+1's DMA (split: its W half), this step's fragments
+      if (pf) {
+        if (split) stage_w(buf ^ 1, kt + 1);
+        else stage(buf ^ 1, kt + 1);
+      }
       read_frags(buf, 0);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       math();
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_barrier" ::: "memory");
-      // READ(kt, 1); own DMA of K-tile kt+1 retired before the barrier
-      read_frags(buf, 1);
-      if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NST) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      // READ(kt, 1); own DMA of K-tile kt+1 retired before the barrier (split: the W
+      // half here, the A half -- read first by this wave half, one segment later --
+      // at the end of MATH(kt, 1))
+      if (pf && split) {
+        stage_a(buf ^ 1, kt + 1);
+        read_frags(buf, 1);
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::AL) : "memory");
+      } else {
+        read_frags(buf, 1);
+        if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NST) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      }
       __builtin_amdgcn_sched_barrier(0);
       math();
       __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_barrier" ::: "memory");
+      if (pf && split) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_barrier" ::: "memory");
     }
     if (wm == 0) asm volatile("s_barrier" ::: "memory");  // balance the stagger
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every read of both buffers retired
@@ -1434,11 +1512,11 @@ inline int ppp_pick_bm(int epi, int M, int N) {
   return r192 * 192 * 10 < r256 * 256 * 9 ? 192 : 256;
 }
 
-template <int EPI, int BMT>
-int launch_ppp_bm(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int M, int N, int K, const Epi& ep,
+template <int EPI, int BMT, bool FK>
+int launch_ppp_fk(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int M, int N, int K, const Epi& ep,
                   hipStream_t s) {
   static bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)gemm_ppp_kernel<EPI, BMT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gemm_ppp_kernel<EPI, BMT, FK>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               PP_LDS_MAX);
     return true;
   }();
@@ -1450,12 +1528,30 @@ int launch_ppp_bm(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, in
   // M-tiles per tile group (VGGT_GEMM_GM overrides; 0 = row-major).  Aggregator
   // step 98.45 -> 97.3-97.6 ms at 4 (8: 97.55, 16: 98.5); fc1 at K = 4096 625 ->
   // 591 us (r3y, r3z)
-  static int gm = [] {
+  static int sched = [] {
     const char* e = getenv("VGGT_GEMM_GM");
-    return e ? atoi(e) : 4;
+    const char* d = getenv("VGGT_GEMM_SPLITDMA");
+    return (e ? atoi(e) & 255 : 4) | (d && !atoi(d) ? 0 : 256);
   }();
-  gemm_ppp_kernel<EPI, BMT><<<nwg, PNT, lds, s>>>(a, lda, w, ldw, M, N, K, ep, gm);
+  gemm_ppp_kernel<EPI, BMT, FK><<<nwg, PNT, lds, s>>>(a, lda, w, ldw, M, N, K, ep, sched);
   return VGGT_OK;
+}
+
+template <int EPI, int BMT>
+int launch_ppp_bm(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int M, int N, int K, const Epi& ep,
+                  hipStream_t s) {
+  // Whole-K-tile READ / MATH segments (VGGT_GEMM_FULLK bits: 1 bf16 / GELU / f32,
+  // 2 qkv, 4 residual; default 5).  In the model (same box, r3x kernel traces):
+  // fc2 + residual 206.6 -> 199.9 us, fc1 + GELU 196.3 -> 193.5 us.  The fused qkv
+  // form keeps the half-K segments: with both halves' fragments live its q/k-norm +
+  // RoPE epilogue spills (256 VGPRs + scratch), +2 ms per step.
+  static int fk = [] {
+    const char* e = getenv("VGGT_GEMM_FULLK");
+    return e ? atoi(e) : 5;
+  }();
+  const int bit = EPI == EPI_QKNORM_D64 ? 2 : EPI == VGGT_EPI_RESID_F32 ? 4 : 1;
+  if (fk & bit) return launch_ppp_fk<EPI, BMT, true>(a, lda, w, ldw, M, N, K, ep, s);
+  return launch_ppp_fk<EPI, BMT, false>(a, lda, w, ldw, M, N, K, ep, s);
 }
 
 template <int EPI>

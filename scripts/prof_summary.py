@@ -16,7 +16,11 @@ def main(path, steps=None):
     for r in rows:
         if r[4] < 0.002 * tot:
             continue
-        print(f"| {r[0][:80]} | {r[1]} | {r[3]} | {r[4]:.2f} | {r[5]:.1f} | {r[6]:.1f} | {r[7]:.1f} | {r[8]} | {r[9]} | {100*r[4]/tot:.1f}% |")
+        name = r[0]
+        if name.startswith("void "):
+            name = name[5:]
+        name = name.replace("(anonymous namespace)::", "").split("(")[0]
+        print(f"| {name[:100]} | {r[1]} | {r[3]} | {r[4]:.2f} | {r[5]:.1f} | {r[6]:.1f} | {r[7]:.1f} | {r[8]} | {r[9]} | {100*r[4]/tot:.1f}% |")
     print(f"\ntotal kernel time {tot:.2f} ms over {sum(r[3] for r in rows)} dispatches")
 
 
