@@ -280,12 +280,35 @@ int vggt_conv2d_bf16x3(const float* x, int64_t ldx, int nimg, int hi, int wi, in
                        int64_t ldy, int relu_in, int relu_out, const float* res1, int64_t ldr1, int res1_relu,
                        const float* res2, int64_t ldr2, const float* pos, int shuffle, void* stream);
 
+/*
+ * vggt_conv2d_bf16x3 on an activation split beforehand (vggt_split_act_bf16x2,
+ * which also applies the input ReLU): x_hi / x_lo bf16 [nimg, hi, wi, ci] with
+ * pixel stride ldx (elements, % 8 == 0), whole map < 2 GiB.  The im2col gather
+ * is LDS-DMA of the bf16 halves (out-of-image taps read as zeros); results are
+ * bitwise equal to vggt_conv2d_bf16x3 with relu_in on the f32 input.  y (f32) and/or
+ * y_hi / y_lo (the NEXT conv's pre-split input: split(split_relu ? max(y, 0) : y),
+ * bf16 rows of stride ldys) are written; either may be NULL, not both.
+ */
+int vggt_conv2d_bf16x3_pre(const void* x_hi, const void* x_lo, int64_t ldx, int nimg, int hi, int wi, int ci,
+                           const void* w_hi, const void* w_lo, const float* bias, int co, int kh, int kw, int stride,
+                           int pad, float* y, int64_t ldy, int relu_out, const float* res1, int64_t ldr1,
+                           int res1_relu, const float* res2, int64_t ldr2, const float* pos, int shuffle,
+                           void* y_hi, void* y_lo, int64_t ldys, int split_relu, void* stream);
+
+/* hi / lo = split(relu ? max(x, 0) : x) of a [rows, cols] f32 map (row stride ldx, cols % 4 == 0)
+ * into contiguous bf16 [rows, cols] maps: hi = bf16(v), lo = bf16(v - hi) (DPT conv inputs). */
+int vggt_split_act_bf16x2(const float* x, int64_t ldx, int64_t rows, int cols, int relu, void* hi, void* lo,
+                          void* stream);
+
 /* hi[i] = bf16(x[i]), lo[i] = bf16(x[i] - hi[i]) for i < n (weight split for vggt_conv2d_bf16x3). */
 int vggt_split_bf16x2(const float* x, int64_t n, void* hi, void* lo, void* stream);
 
 /* NHWC bilinear resize with align_corners=True (custom_interpolate, dpt_head ext), + optional pos table. */
 int vggt_upsample_bilinear_f32(const float* x, int nimg, int hi, int wi, int C, float* y, int ho, int wo,
                                const float* pos, void* stream);
+/* Same, writing y (f32, may be NULL) and/or the split bf16 halves of relu?(y) (contiguous [.., C]). */
+int vggt_upsample_bilinear_split(const float* x, int nimg, int hi, int wi, int C, float* y, int ho, int wo,
+                                 const float* pos, void* y_hi, void* y_lo, int split_relu, void* stream);
 
 /*
  * DPT activate_head (ext): x [npix, ncl] NHWC with the confidence last;

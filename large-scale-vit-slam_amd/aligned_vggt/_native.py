@@ -52,6 +52,10 @@ _SIGS = {
     "vggt_conv2d_bf16x3": [_vp, _i64, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _i64, _i, _i, _vp, _i64,
                            _i, _vp, _i64, _vp, _i, _vp],
     "vggt_split_bf16x2": [_vp, _i64, _vp, _vp, _vp],
+    "vggt_conv2d_bf16x3_pre": [_vp, _vp, _i64, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _i64, _i, _vp,
+                               _i64, _i, _vp, _i64, _vp, _i, _vp, _vp, _i64, _i, _vp],
+    "vggt_upsample_bilinear_split": [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _i, _vp],
+    "vggt_split_act_bf16x2": [_vp, _i64, _i64, _i, _i, _vp, _vp, _vp],
     "vggt_upsample_bilinear_f32": [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp],
     "vggt_dpt_activate": [_vp, _i64, _i64, _i, _i, _i, _vp, _vp, _vp, _vp],
     "vggt_irls_sim3": [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i, _i64, _f, _f, _i, _f, _vp, _vp, _vp, _vp,
@@ -420,6 +424,47 @@ def conv2d_bf16x3(x: torch.Tensor, nimg: int, hi: int, wi: int, ci: int, w_hi: t
                                   _ld(res2) if res2 is not None else 0, _p(pos), shuffle, _stream())
     _check(rc, "vggt_conv2d_bf16x3")
     return y
+
+
+def conv2d_bf16x3_pre(x_hi: torch.Tensor, x_lo: torch.Tensor, nimg: int, hi: int, wi: int, ci: int,
+                      w_hi: torch.Tensor, w_lo: torch.Tensor, bias, co: int, kh: int, kw: int, stride: int, pad: int,
+                      y: torch.Tensor, relu_out: bool = False, res1: Optional[torch.Tensor] = None,
+                      res1_relu: bool = False, res2: Optional[torch.Tensor] = None, pos: Optional[torch.Tensor] = None,
+                      shuffle: int = 0, y_split=None, split_relu: bool = False):
+    """conv2d_bf16x3 on an activation pre-split by split_act_bf16x2 (LDS-DMA gather).
+    y (f32) and/or y_split = (hi, lo) bf16 (the next conv's split input) are written."""
+    _dev(x_hi, "conv2d_bf16x3_pre")
+    yh, yl = y_split if y_split is not None else (None, None)
+    rc = lib().vggt_conv2d_bf16x3_pre(_p(x_hi), _p(x_lo), _ld(x_hi), nimg, hi, wi, ci, _p(w_hi), _p(w_lo), _p(bias), co,
+                                      kh, kw, stride, pad, _p(y), _ld(y) if y is not None else 0, int(relu_out),
+                                      _p(res1), _ld(res1) if res1 is not None else 0, int(res1_relu), _p(res2),
+                                      _ld(res2) if res2 is not None else 0, _p(pos), shuffle, _p(yh), _p(yl),
+                                      _ld(yh) if yh is not None else 0, int(split_relu), _stream())
+    _check(rc, "vggt_conv2d_bf16x3_pre")
+    return y
+
+
+def upsample_bilinear_split(x: torch.Tensor, nimg: int, hi: int, wi: int, C: int, y, ho: int, wo: int,
+                            pos: Optional[torch.Tensor] = None, y_split=None, split_relu: bool = False):
+    """upsample_bilinear_f32 writing y (may be None) and/or the split halves of relu?(y)."""
+    _dev(x, "upsample_bilinear_split")
+    yh, yl = y_split if y_split is not None else (None, None)
+    rc = lib().vggt_upsample_bilinear_split(_p(x), nimg, hi, wi, C, _p(y), ho, wo, _p(pos), _p(yh), _p(yl),
+                                            int(split_relu), _stream())
+    _check(rc, "vggt_upsample_bilinear_split")
+
+
+def split_act_bf16x2(x: torch.Tensor, relu: bool = False, out=None):
+    """(hi, lo) bf16 [rows, cols] maps of relu?(x) for a 2-D f32 row view x."""
+    _dev(x, "split_act_bf16x2")
+    rows, cols = x.shape
+    if out is None:
+        out = (torch.empty(rows, cols, dtype=torch.bfloat16, device=x.device),
+               torch.empty(rows, cols, dtype=torch.bfloat16, device=x.device))
+    hi, lo = out
+    _check(lib().vggt_split_act_bf16x2(_p(x), _ld(x), rows, cols, int(relu), _p(hi), _p(lo), _stream()),
+           "vggt_split_act_bf16x2")
+    return hi, lo
 
 
 def split_bf16x2(x: torch.Tensor):

@@ -2,8 +2,10 @@
 at featureAligned_vggt.py:166, point head at :183 / pointAligned :70) on the
 HIP fp32 tier (autocast disabled in the reference, featureAligned_vggt.py:104).
 
-All activations are NHWC fp32 rows in HBM; every convolution is one
-vggt_conv2d_f32 launch (exact-f32 MFMA implicit GEMM) with the surrounding
+All activations are NHWC rows in HBM -- fp32 where a residual or an upsample
+reads them, else only as the split bf16 halves (hi, lo) the next convolution
+gathers; every convolution is one implicit-GEMM launch (split-bf16 on the bf16
+matrix path by default, or exact-f32 MFMA, VGGT_CONV=fp32) with the surrounding
 elementwise work fused into it: the positional embedding add after the 1x1
 projections, the stride==kernel ConvTranspose2d as a pixel-shuffle store,
 the in-place-ReLU semantics of ResidualConvUnit (relu on the conv input,
@@ -93,9 +95,16 @@ def _scratch(in_shape, out_shape) -> nn.Module:
     return s
 
 
-# DPT convolutions: "bf16x3" (split-bf16 operands on the bf16 matrix path,
-# ~2^-16 relative per product; default) or "fp32" (exact f32 MFMA).
-CONV_PRECISION = os.environ.get("VGGT_CONV", "bf16x3")
+# DPT convolutions: "bf16x3pre" (default: split-bf16 operands on the bf16 matrix
+# path, the activation split once by its producer -- conv epilogue, upsample or a
+# split pass -- and gathered by LDS-DMA), "bf16x3" (the same products with the
+# split done in the conv's register-staged gather; bitwise equal) or "fp32"
+# (exact f32 MFMA).
+CONV_PRECISION = os.environ.get("VGGT_CONV", "bf16x3pre")
+
+
+def _pre() -> bool:
+    return CONV_PRECISION == "bf16x3pre"
 
 
 def _pack_conv(conv: nn.Module, transpose: bool = False):
@@ -125,52 +134,84 @@ def _pack_conv(conv: nn.Module, transpose: bool = False):
     return c[1:]
 
 
-def _conv_call(x_t, n, h, w_, c, packed, co, kh, kw, stride, pad, y, relu_in=False, relu_out=False, res1=None,
+class _Map:
+    """An NHWC activation: rows [n*h*w, c] fp32 (``t``) and/or its split bf16
+    halves ``sp`` = (hi, lo) of relu(x) (``sp_relu``) or of x -- the form the
+    next convolution gathers."""
+
+    __slots__ = ("t", "n", "h", "w", "c", "sp", "sp_relu")
+
+    def __init__(self, t, n, h, w, c, sp=None, sp_relu=False):
+        self.t, self.n, self.h, self.w, self.c = t, n, h, w, c
+        self.sp, self.sp_relu = sp, sp_relu
+
+
+def _split_of(x: _Map, relu: bool):
+    if x.sp is not None and x.sp_relu == relu:
+        return x.sp
+    assert x.t is not None, "DPT map has neither its f32 rows nor the split this conv needs"
+    return N.split_act_bf16x2(x.t, relu)
+
+
+def _outputs(rows: int, co: int, dev, f32: bool, split):
+    """(y, y_split) buffers for a producer: split None / "plain" / "relu"."""
+    if not _pre():
+        f32, split = True, None
+    y = torch.empty(rows, co, device=dev) if f32 else None
+    ys = None
+    if split is not None:
+        ys = (torch.empty(rows, co, device=dev, dtype=torch.bfloat16),
+              torch.empty(rows, co, device=dev, dtype=torch.bfloat16))
+    return y, ys
+
+
+def _conv_call(x: _Map, packed, co, kh, kw, stride, pad, y, ys, split_relu, relu_in=False, relu_out=False, res1=None,
                res1_relu=False, res2=None, pos=None, shuffle=0):
     wp, b, w_hi, w_lo = packed
+    n, h, w_, c = x.n, x.h, x.w, x.c
     if CONV_PRECISION == "fp32":
-        N.conv2d_f32(x_t, n, h, w_, c, wp, b, co, kh, kw, stride, pad, y, relu_in, relu_out, res1, res1_relu, res2,
+        N.conv2d_f32(x.t, n, h, w_, c, wp, b, co, kh, kw, stride, pad, y, relu_in, relu_out, res1, res1_relu, res2,
                      pos, shuffle=shuffle)
+    elif _pre():
+        xh, xl = _split_of(x, relu_in)
+        N.conv2d_bf16x3_pre(xh, xl, n, h, w_, c, w_hi, w_lo, b, co, kh, kw, stride, pad, y, relu_out, res1, res1_relu,
+                            res2, pos, shuffle=shuffle, y_split=ys, split_relu=split_relu)
     else:
-        N.conv2d_bf16x3(x_t, n, h, w_, c, w_hi, w_lo, b, co, kh, kw, stride, pad, y, relu_in, relu_out, res1,
+        N.conv2d_bf16x3(x.t, n, h, w_, c, w_hi, w_lo, b, co, kh, kw, stride, pad, y, relu_in, relu_out, res1,
                         res1_relu, res2, pos, shuffle=shuffle)
 
 
-class _Map:
-    """An NHWC activation: rows [n*h*w, c] fp32."""
-
-    __slots__ = ("t", "n", "h", "w", "c")
-
-    def __init__(self, t, n, h, w, c):
-        self.t, self.n, self.h, self.w, self.c = t, n, h, w, c
-
-
 def _conv(x: _Map, conv: nn.Conv2d, stride=1, pad=None, relu_in=False, relu_out=False, res1: _Map = None,
-          res1_relu=False, res2: _Map = None, pos=None) -> _Map:
+          res1_relu=False, res2: _Map = None, pos=None, f32=True, split=None) -> _Map:
+    """split: the consumer's gather form to write besides (or, f32=False, instead
+    of) the f32 rows -- None, "plain" or "relu" (the consumer's relu_in)."""
     packed = _pack_conv(conv)
     co, _, kh, kw = conv.weight.shape
     pad = conv.padding[0] if pad is None else pad
     ho = (x.h + 2 * pad - kh) // stride + 1
     wo = (x.w + 2 * pad - kw) // stride + 1
-    y = torch.empty(x.n * ho * wo, co, device=x.t.device)
-    _conv_call(x.t, x.n, x.h, x.w, x.c, packed, co, kh, kw, stride, pad, y, relu_in, relu_out,
+    y, ys = _outputs(x.n * ho * wo, co, x.t.device if x.t is not None else x.sp[0].device, f32, split)
+    _conv_call(x, packed, co, kh, kw, stride, pad, y, ys, split == "relu", relu_in, relu_out,
                res1.t if res1 else None, res1_relu, res2.t if res2 else None, pos)
-    return _Map(y, x.n, ho, wo, co)
+    return _Map(y, x.n, ho, wo, co, ys, split == "relu")
 
 
-def _convT(x: _Map, conv: nn.ConvTranspose2d) -> _Map:
+def _convT(x: _Map, conv: nn.ConvTranspose2d, f32=True, split=None) -> _Map:
     packed = _pack_conv(conv, transpose=True)
     ci, co, k, _ = conv.weight.shape
     assert conv.stride[0] == k and conv.padding[0] == 0
-    y = torch.empty(x.n * x.h * k * x.w * k, co, device=x.t.device)
-    _conv_call(x.t, x.n, x.h, x.w, x.c, packed, co, 1, 1, 1, 0, y, shuffle=k)
-    return _Map(y, x.n, x.h * k, x.w * k, co)
+    y, ys = _outputs(x.n * x.h * k * x.w * k, co, x.t.device if x.t is not None else x.sp[0].device, f32, split)
+    _conv_call(x, packed, co, 1, 1, 1, 0, y, ys, split == "relu", shuffle=k)
+    return _Map(y, x.n, x.h * k, x.w * k, co, ys, split == "relu")
 
 
-def _upsample(x: _Map, ho: int, wo: int, pos=None) -> _Map:
-    y = torch.empty(x.n * ho * wo, x.c, device=x.t.device)
-    N.upsample_bilinear_f32(x.t, x.n, x.h, x.w, x.c, y, ho, wo, pos)
-    return _Map(y, x.n, ho, wo, x.c)
+def _upsample(x: _Map, ho: int, wo: int, pos=None, f32=True, split=None) -> _Map:
+    y, ys = _outputs(x.n * ho * wo, x.c, x.t.device, f32, split)
+    if ys is None:
+        N.upsample_bilinear_f32(x.t, x.n, x.h, x.w, x.c, y, ho, wo, pos)
+    else:
+        N.upsample_bilinear_split(x.t, x.n, x.h, x.w, x.c, y, ho, wo, pos, y_split=ys, split_relu=split == "relu")
+    return _Map(y, x.n, ho, wo, x.c, ys, split == "relu")
 
 
 class DPTHead(nn.Module):
@@ -218,15 +259,18 @@ class DPTHead(nn.Module):
             cache[key] = pos_table(C, h, w, W_img, H_img).to(device)
         return cache[key]
 
-    def _fuse(self, blk: FeatureFusionBlock, x0: _Map, x1: Optional[_Map], size) -> _Map:
+    def _fuse(self, blk: FeatureFusionBlock, x0: _Map, x1: Optional[_Map], size, f32=True, split=None) -> _Map:
+        """x1 (and x0 when x1 is None) arrive with their f32 rows and the ReLU'd split;
+        (f32, split) select the output forms for the consumer."""
         out = x0
         if x1 is not None:
-            t = _conv(x1, blk.resConfUnit1.conv1, relu_in=True, relu_out=True)
-            out = _conv(t, blk.resConfUnit1.conv2, res1=x1, res1_relu=True, res2=x0)
-        t = _conv(out, blk.resConfUnit2.conv1, relu_in=True, relu_out=True)
+            t = _conv(x1, blk.resConfUnit1.conv1, relu_in=True, relu_out=True, f32=False, split="plain")
+            out = _conv(t, blk.resConfUnit1.conv2, res1=x1, res1_relu=True, res2=x0, split="relu")
+        t = _conv(out, blk.resConfUnit2.conv1, relu_in=True, relu_out=True, f32=False, split="plain")
         out = _conv(t, blk.resConfUnit2.conv2, res1=out, res1_relu=True)
         ho, wo = size if size is not None else (out.h * 2, out.w * 2)
-        return _conv(_upsample(out, ho, wo), blk.out_conv)
+        up = _upsample(out, ho, wo, f32=False, split="plain")
+        return _conv(up, blk.out_conv, f32=f32, split=split)
 
     @torch.no_grad()
     def forward(self, aggregated_tokens_list: List[torch.Tensor], images: torch.Tensor, patch_start_idx: int,
@@ -251,25 +295,28 @@ class DPTHead(nn.Module):
                                 Cin, hw, P, patch_start_idx, hw, 0)
             oc = self.out_channels[li]
             pos = self._pos(oc, ph, pw, W, H, dev) if self.pos_embed else None
-            x = _conv(_Map(xl, F_, ph, pw, Cin), self.projects[li], pos=pos)
+            # every producer below writes the form its consumer gathers (f32 rows only
+            # where a residual / upsample reads them)
+            x = _conv(_Map(xl, F_, ph, pw, Cin), self.projects[li], pos=pos, f32=False, split="plain")
             if li == 0 or li == 1:
-                x = _convT(x, self.resize_layers[li])
+                x = _convT(x, self.resize_layers[li], f32=False, split="plain")
             elif li == 3:
-                x = _conv(x, self.resize_layers[3], stride=2, pad=1)
+                x = _conv(x, self.resize_layers[3], stride=2, pad=1, f32=False, split="plain")
             feats.append(x)
         sc = self.scratch
-        l1 = _conv(feats[0], sc.layer1_rn)
-        l2 = _conv(feats[1], sc.layer2_rn)
-        l3 = _conv(feats[2], sc.layer3_rn)
-        l4 = _conv(feats[3], sc.layer4_rn)
+        l1 = _conv(feats[0], sc.layer1_rn, split="relu")
+        l2 = _conv(feats[1], sc.layer2_rn, split="relu")
+        l3 = _conv(feats[2], sc.layer3_rn, split="relu")
+        l4 = _conv(feats[3], sc.layer4_rn, split="relu")
         out = self._fuse(sc.refinenet4, l4, None, (l3.h, l3.w))
         out = self._fuse(sc.refinenet3, out, l3, (l2.h, l2.w))
         out = self._fuse(sc.refinenet2, out, l2, (l1.h, l1.w))
-        out = self._fuse(sc.refinenet1, out, l1, None)
+        out = self._fuse(sc.refinenet1, out, l1, None, f32=False, split="plain")
         out = _conv(out, sc.output_conv1)
         Ho, Wo = int(ph * self.patch_size / self.down_ratio), int(pw * self.patch_size / self.down_ratio)
-        out = _upsample(out, Ho, Wo, self._pos(out.c, Ho, Wo, W, H, dev) if self.pos_embed else None)
-        out = _conv(out, sc.output_conv2[0], relu_out=True)
+        out = _upsample(out, Ho, Wo, self._pos(out.c, Ho, Wo, W, H, dev) if self.pos_embed else None, f32=False,
+                        split="plain")
+        out = _conv(out, sc.output_conv2[0], relu_out=True, f32=False, split="plain")
         out = _conv(out, sc.output_conv2[2])
         ncl = self.output_dim
         npix = F_ * Ho * Wo

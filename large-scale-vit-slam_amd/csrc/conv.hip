@@ -36,6 +36,11 @@ struct ConvArgs {
   int relu_in, relu_out, res1_relu;
   int shuffle;  // >0: ConvT pixel shuffle factor s; co is then the per-tap output channels
   int ncols;    // GEMM N (= co, or s*s*co for the shuffle)
+  // optional split output (the next conv's pre-split input): yh / yl = split(relu?(y))
+  bf16_t* yh;
+  bf16_t* yl;
+  int64_t ldys;
+  int split_relu;
 };
 
 // ---- shared epilogue: lane holds C[m = 4q + i][n = r16] of each 16x16 tile;
@@ -77,7 +82,13 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const f32x4 (&a
           }
           if (a.res2) v += a.res2[(int64_t)m * a.ldr2 + co];
         }
-        a.y[opix * a.ldy + co] = v;
+        if (a.y) a.y[opix * a.ldy + co] = v;
+        if (a.yh) {
+          const float sv = a.split_relu ? fmaxf(v, 0.f) : v;
+          const float hv = round_bf(sv);
+          a.yh[opix * a.ldys + co] = f2bf(hv);
+          a.yl[opix * a.ldys + co] = f2bf(sv - hv);
+        }
       }
   }
 }
@@ -472,6 +483,167 @@ __global__ __launch_bounds__(NT, 2) void conv_bf16x3_kernel(ConvArgs a, const bf
   conv_epilogue<NTN>(a, acc, M, m0, n0, wm, wn, r16, q);
 }
 
+// ===========================================================================
+// Pre-split form (vggt_conv2d_bf16x3_pre): the activation arrives already
+// split into bf16 hi / lo maps (vggt_split_act_bf16x2, input ReLU applied
+// there), so the im2col gather is LDS-DMA like the weights -- per lane one
+// 16-B piece of a 64-B (32-channel) pixel row, out-of-image taps get an offset
+// past num_records and land as zeros.  The register-staged form above spends
+// ~230 VALU instructions per wave per K-step on the gather addressing, the
+// split and the LDS stores (4.75 per MFMA, VALU-issue-bound at 34% MFMA busy,
+// 148^2 x 256 -> 256: profiles r3c); here the K-step is 8 DMA pieces and two
+// address selects per wave.  Same K order, same MFMA sequence: bitwise equal
+// to conv_bf16x3_kernel.
+// ===========================================================================
+template <int BNX>
+__global__ __launch_bounds__(NT, 2) void conv_pre_kernel(ConvArgs a, const bf16_t* __restrict__ xhi,
+                                                         const bf16_t* __restrict__ xlo, uint32_t xbytes,
+                                                         const bf16_t* __restrict__ whi, const bf16_t* __restrict__ wlo) {
+  constexpr int NTN = BNX / 32;
+  constexpr int AT = BM * BK * 2, WT = BNX * BK * 2;
+  constexpr int STG = 2 * AT + 2 * WT;  // Ahi, Alo, Whi, Wlo
+  constexpr int WPW = WT / 1024 / 4 > 0 ? WT / 1024 / 4 : 1;
+  constexpr int APW = AT / 1024 / 4;  // A pieces per wave per half (2)
+  __shared__ __attribute__((aligned(16))) char smem[2 * STG];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int M = a.nimg * a.ho * a.wo;
+  const int tiles_n = (a.ncols + BNX - 1) / BNX;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (t / tiles_n) * BM;
+  const int n0 = (t % tiles_n) * BNX;
+  const int K = a.kh * a.kw * a.ci;
+  const int nk = K / BK;
+  const int ntap = a.kh * a.kw;
+  auto kcol = [&](int s) { return (s % ntap) * a.ci + (s / ntap) * BK; };
+
+  // A pieces: rows (wave*APW + j)*16 + lane/4, LDS chunk lane%4 <- global chunk swz64(row, lane%4)
+  int pb[APW], py[APW], px[APW];
+#pragma unroll
+  for (int j = 0; j < APW; ++j) {
+    const int row = (wave * APW + j) * 16 + (lane >> 2);
+    const int m = m0 + row;
+    const int mm = m < M ? m : 0;
+    const int img = mm / (a.ho * a.wo), rem = mm % (a.ho * a.wo);
+    py[j] = (rem / a.wo) * a.stride - a.pad;
+    px[j] = (rem % a.wo) * a.stride - a.pad;
+    pb[j] = ((img * a.hi + py[j]) * a.wi + px[j]) * (int)a.ldx + swz64(row, lane & 3) * 8;
+    if (m >= M) py[j] = -(1 << 20);  // rows past M: never inside the image (read as zeros)
+  }
+  uint32_t woff[WPW];
+#pragma unroll
+  for (int i = 0; i < WPW; ++i) {
+    const int row = (wave * WPW + i) * 16 + (lane >> 2);
+    woff[i] = (uint32_t)(row * K + swz64(row, lane & 3) * 8) * 2u;
+  }
+  const bool wdma = wave * WPW * 1024 < WT;
+  auto rsrc = [](const void* p, uint32_t bytes) {
+    int32x4c r;
+    const uint64_t b = (uint64_t)p;
+    r[0] = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    r[1] = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) & 0xffff;
+    r[2] = (int)bytes;
+    r[3] = 0x00020000;
+    return r;
+  };
+  const int32x4c rwh = rsrc(whi + (int64_t)n0 * K, 0xffffffffu), rwl = rsrc(wlo + (int64_t)n0 * K, 0xffffffffu);
+  const int32x4c rxh = rsrc(xhi, xbytes), rxl = rsrc(xlo, xbytes);
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem));
+  auto stage = [&](int buf, int kt) {
+    const uint32_t b = lds0 + buf * STG;
+    const int tap = kt % ntap, ky = tap / a.kw, kx = tap % a.kw;
+    const int sh = (ky * a.wi + kx) * (int)a.ldx + (kt / ntap) * BK;  // wave-uniform element shift
+#pragma unroll
+    for (int j = 0; j < APW; ++j) {
+      const int iy = py[j] + ky, ix = px[j] + kx;
+      const bool ok = (unsigned)iy < (unsigned)a.hi && (unsigned)ix < (unsigned)a.wi;
+      const uint32_t off = ok ? (uint32_t)(pb[j] + sh) * 2u : 0xfffffff0u;
+      cdma16(rxh, off, 0, b + (wave * APW + j) * 1024);
+      cdma16(rxl, off, 0, b + AT + (wave * APW + j) * 1024);
+    }
+    if (wdma) {
+      const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(kcol(kt) * 2));
+#pragma unroll
+      for (int i = 0; i < WPW; ++i) {
+        cdma16(rwh, woff[i], soff, b + 2 * AT + (wave * WPW + i) * 1024);
+        cdma16(rwl, woff[i], soff, b + 2 * AT + WT + (wave * WPW + i) * 1024);
+      }
+    }
+  };
+
+  const int wm = wave >> 1, wn = wave & 1;
+  const int r16 = lane & 15, q = lane >> 4;
+  const int roff = r16 * 64 + (swz64(r16, q) << 4);
+  f32x4 acc[4][NTN];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NTN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int cur) {
+    const char* base = smem + cur * STG;
+    bf16x8 ah[4], al[4], bh[NTN], bl[NTN];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int o = (wm * 64 + mt * 16) * 64 + roff;
+      ah[mt] = *(const bf16x8*)(base + o);
+      al[mt] = *(const bf16x8*)(base + AT + o);
+    }
+#pragma unroll
+    for (int nt = 0; nt < NTN; ++nt) {
+      const int o = (wn * NTN * 16 + nt * 16) * 64 + roff;
+      bh[nt] = *(const bf16x8*)(base + 2 * AT + o);
+      bl[nt] = *(const bf16x8*)(base + 2 * AT + WT + o);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NTN; ++nt) {
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[mt], bh[nt], acc[mt][nt], 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mt], bl[nt], acc[mt][nt], 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mt], bh[nt], acc[mt][nt], 0, 0, 0);
+      }
+  };
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+    compute(cur);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  conv_epilogue<NTN>(a, acc, M, m0, n0, wm, wn, r16, q);
+}
+
+// hi / lo = split(relu?(x)) of a [rows, cols] f32 map with row stride ldx
+// (cols % 4 == 0) into contiguous [rows, cols] bf16 maps
+__global__ __launch_bounds__(256) void split_act_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows, int cols,
+                                                        int relu, bf16_t* __restrict__ hi, bf16_t* __restrict__ lo) {
+  const int c4n = cols / 4;
+  const int64_t total = rows * c4n;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / c4n;
+    const int c = (int)(i - r * c4n) * 4;
+    f32x4 v = *(const f32x4*)(x + r * ldx + c);
+    float h[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (relu) v[j] = fmaxf(v[j], 0.f);
+      h[j] = round_bf(v[j]);
+    }
+    uint2 ph, pl;
+    ph.x = pack_bf2(h[0], h[1]);
+    ph.y = pack_bf2(h[2], h[3]);
+    pl.x = pack_bf2(v[0] - h[0], v[1] - h[1]);
+    pl.y = pack_bf2(v[2] - h[2], v[3] - h[3]);
+    *(uint2*)(hi + r * cols + c) = ph;
+    *(uint2*)(lo + r * cols + c) = pl;
+  }
+}
+
 __global__ __launch_bounds__(256) void split_bf16x2_kernel(const float* __restrict__ x, int64_t n, bf16_t* __restrict__ hi,
                                                            bf16_t* __restrict__ lo) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -486,7 +658,8 @@ __global__ __launch_bounds__(256) void split_bf16x2_kernel(const float* __restri
 // optional positional table [ho*wo, C] added to the result.
 __global__ __launch_bounds__(256) void upsample_kernel(const float* __restrict__ x, int nimg, int hi, int wi, int C,
                                                        float* __restrict__ y, int ho, int wo,
-                                                       const float* __restrict__ pos) {
+                                                       const float* __restrict__ pos, bf16_t* __restrict__ yh,
+                                                       bf16_t* __restrict__ yl, int split_relu) {
   const int c4n = C / 4;
   const int64_t total = (int64_t)nimg * ho * wo * c4n;
   const float sh = ho > 1 ? (float)(hi - 1) / (float)(ho - 1) : 0.f;
@@ -509,7 +682,22 @@ __global__ __launch_bounds__(256) void upsample_kernel(const float* __restrict__
     const f32x4 v11 = *(const f32x4*)(b + ((int64_t)y1 * wi + x1) * C + c);
     f32x4 o = hy * (hx * v00 + lx * v01) + ly * (hx * v10 + lx * v11);
     if (pos) o += *(const f32x4*)(pos + (int64_t)rem * C + c);
-    *(f32x4*)(y + p * C + c) = o;
+    if (y) *(f32x4*)(y + p * C + c) = o;
+    if (yh) {
+      float h[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (split_relu) o[j] = fmaxf(o[j], 0.f);
+        h[j] = round_bf(o[j]);
+      }
+      uint2 ph, pl;
+      ph.x = pack_bf2(h[0], h[1]);
+      ph.y = pack_bf2(h[2], h[3]);
+      pl.x = pack_bf2(o[0] - h[0], o[1] - h[1]);
+      pl.y = pack_bf2(o[2] - h[2], o[3] - h[3]);
+      *(uint2*)(yh + p * C + c) = ph;
+      *(uint2*)(yl + p * C + c) = pl;
+    }
   }
 }
 
@@ -556,6 +744,9 @@ extern "C" int vggt_conv2d_f32(const float* x, int64_t ldx, int nimg, int hi, in
   a.relu_in = relu_in; a.relu_out = relu_out; a.res1_relu = res1_relu;
   a.shuffle = shuffle;
   a.ncols = shuffle ? shuffle * shuffle * co : co;
+  a.yh = a.yl = nullptr;
+  a.ldys = 0;
+  a.split_relu = 0;
   const int64_t M = (int64_t)nimg * a.ho * a.wo;
   const int64_t nwg = ((M + BM - 1) / BM) * ((a.ncols + BN - 1) / BN);
   if (nwg > 0x7fffffff) return VGGT_ERR_SHAPE;
@@ -582,6 +773,9 @@ static int conv_args(ConvArgs& a, const float* x, int64_t ldx, int nimg, int hi,
   a.relu_in = relu_in; a.relu_out = relu_out; a.res1_relu = res1_relu;
   a.shuffle = shuffle;
   a.ncols = shuffle ? shuffle * shuffle * co : co;
+  a.yh = a.yl = nullptr;
+  a.ldys = 0;
+  a.split_relu = 0;
   const int64_t M = (int64_t)nimg * a.ho * a.wo;
   *nwg = ((M + BM - 1) / BM) * ((a.ncols + BN - 1) / BN);
   if (*nwg > 0x7fffffff) return VGGT_ERR_SHAPE;
@@ -623,6 +817,53 @@ extern "C" int vggt_conv2d_bf16x3(const float* x, int64_t ldx, int nimg, int hi,
   return VGGT_OK;
 }
 
+extern "C" int vggt_conv2d_bf16x3_pre(const void* x_hi, const void* x_lo, int64_t ldx, int nimg, int hi, int wi,
+                                      int ci, const void* w_hi, const void* w_lo, const float* bias, int co, int kh,
+                                      int kw, int stride, int pad, float* y, int64_t ldy, int relu_out,
+                                      const float* res1, int64_t ldr1, int res1_relu, const float* res2, int64_t ldr2,
+                                      const float* pos, int shuffle, void* y_hi, void* y_lo, int64_t ldys,
+                                      int split_relu, void* stream) {
+  ConvArgs a;
+  int64_t nwg;
+  const int rc = conv_args(a, (const float*)x_hi, ldx, nimg, hi, wi, ci, nullptr, bias, co, kh, kw, stride, pad, y, ldy,
+                           0, relu_out, res1, ldr1, res1_relu, res2, ldr2, pos, shuffle, &nwg);
+  if (rc) return rc;
+  if (!y && !y_hi) return VGGT_ERR_SHAPE;
+  if (!y_hi != !y_lo || (y_hi && ldys < co)) return VGGT_ERR_SHAPE;
+  a.yh = (bf16_t*)y_hi;
+  a.yl = (bf16_t*)y_lo;
+  a.ldys = ldys;
+  a.split_relu = split_relu;
+  if (((uintptr_t)x_lo % 16) || ((uintptr_t)w_hi % 16) || ((uintptr_t)w_lo % 16) || (ldx % 8)) return VGGT_ERR_ALIGN;
+  // 32-bit byte offsets: the whole map (plus the widest tap shift) below 4 GiB
+  const int64_t xb = ((int64_t)nimg * hi * wi - 1) * ldx * 2 + (int64_t)ci * 2;
+  if (xb >= (int64_t)0x7fffff00ll) return VGGT_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  const bf16_t *xh = (const bf16_t*)x_hi, *xl = (const bf16_t*)x_lo;
+  const bf16_t *wh = (const bf16_t*)w_hi, *wl = (const bf16_t*)w_lo;
+  if (a.ncols >= 128) {
+    const int64_t nw2 = (nwg / ((a.ncols + BN - 1) / BN)) * ((a.ncols + 127) / 128);
+    conv_pre_kernel<128><<<(int)nw2, NT, 0, s>>>(a, xh, xl, (uint32_t)xb, wh, wl);
+  } else if (a.ncols > 32) {
+    conv_pre_kernel<64><<<(int)nwg, NT, 0, s>>>(a, xh, xl, (uint32_t)xb, wh, wl);
+  } else {
+    conv_pre_kernel<32><<<(int)nwg, NT, 0, s>>>(a, xh, xl, (uint32_t)xb, wh, wl);
+  }
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+extern "C" int vggt_split_act_bf16x2(const float* x, int64_t ldx, int64_t rows, int cols, int relu, void* hi, void* lo,
+                                     void* stream) {
+  if (rows < 0 || cols <= 0 || cols % 4 || ldx < cols) return VGGT_ERR_SHAPE;
+  if ((ldx % 4) || ((uintptr_t)x % 16) || ((uintptr_t)hi % 8) || ((uintptr_t)lo % 8)) return VGGT_ERR_ALIGN;
+  if (rows == 0) return VGGT_OK;
+  split_act_kernel<<<grid_for(rows * (cols / 4)), 256, 0, (hipStream_t)stream>>>(x, ldx, rows, cols, relu,
+                                                                              (bf16_t*)hi, (bf16_t*)lo);
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
 extern "C" int vggt_split_bf16x2(const float* x, int64_t n, void* hi, void* lo, void* stream) {
   if (n < 0) return VGGT_ERR_SHAPE;
   if (n == 0) return VGGT_OK;
@@ -636,7 +877,19 @@ extern "C" int vggt_upsample_bilinear_f32(const float* x, int nimg, int hi, int 
   if (nimg <= 0 || hi <= 0 || wi <= 0 || ho <= 0 || wo <= 0 || C % 4) return VGGT_ERR_SHAPE;
   if (((uintptr_t)x | (uintptr_t)y) % 16) return VGGT_ERR_ALIGN;
   upsample_kernel<<<grid_for((int64_t)nimg * ho * wo * (C / 4)), 256, 0, (hipStream_t)stream>>>(x, nimg, hi, wi, C, y,
-                                                                                                 ho, wo, pos);
+                                                                                                 ho, wo, pos, nullptr,
+                                                                                                 nullptr, 0);
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+extern "C" int vggt_upsample_bilinear_split(const float* x, int nimg, int hi, int wi, int C, float* y, int ho, int wo,
+                                            const float* pos, void* y_hi, void* y_lo, int split_relu, void* stream) {
+  if (nimg <= 0 || hi <= 0 || wi <= 0 || ho <= 0 || wo <= 0 || C % 4 || (!y && !y_hi) || (!y_hi != !y_lo))
+    return VGGT_ERR_SHAPE;
+  if (((uintptr_t)x | (uintptr_t)y) % 16 || ((uintptr_t)y_hi | (uintptr_t)y_lo) % 8) return VGGT_ERR_ALIGN;
+  upsample_kernel<<<grid_for((int64_t)nimg * ho * wo * (C / 4)), 256, 0, (hipStream_t)stream>>>(
+      x, nimg, hi, wi, C, y, ho, wo, pos, (bf16_t*)y_hi, (bf16_t*)y_lo, split_relu);
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
 }

@@ -25,4 +25,10 @@ for (n, hw, ci, co) in [(16, 148, 256, 256), (16, 296, 256, 128), (16, 74, 256, 
         print(f"conv3x3 n={n} hw={hw} ci={ci} co={co} pf2={pf2}: {us:.1f} us  alg {fl/us/1e6:.0f} TF/s  "
               f"mfma {3*fl/us/1e6:.0f} TF/s", flush=True)
     print("  pf2 == one-deep bitwise:", torch.equal(outs[0], outs[1]), flush=True)
+    xs = N.split_act_bf16x2(x)
+    us = timeit(lambda: N.conv2d_bf16x3_pre(xs[0], xs[1], n, hw, hw, ci, whi, wlo, b, co, 3, 3, 1, 1, y))
+    print(f"conv3x3 n={n} hw={hw} ci={ci} co={co} pre-split: {us:.1f} us  alg {fl/us/1e6:.0f} TF/s  "
+          f"mfma {3*fl/us/1e6:.0f} TF/s  (== register-staged: {torch.equal(y, outs[1])})", flush=True)
+    us = timeit(lambda: N.split_act_bf16x2(x, True, out=xs))
+    print(f"  split pass: {us:.1f} us", flush=True)
     N.tune(N.TUNE_CONV_PF2, 1)

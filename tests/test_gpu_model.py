@@ -108,6 +108,27 @@ def test_heads_fp32_tier_tight(models):
     assert _rel(d, d_ref) < 1e-4 and _rel(c, c_ref) < 1e-4
 
 
+def test_dpt_presplit_bitwise(models):
+    """The pre-split DPT path (each producer writes the split halves its consumer
+    gathers) is bitwise equal to the register-staged split form."""
+    m, sd = models
+    from aligned_vggt.backbone import dpt_head as D
+    from aligned_vggt.utils.synthetic import synthetic_images
+    imgs = synthetic_images(1, 2, 56, 70, seed=4)
+    toks, psi = O.aggregator(sd, imgs, bf16=True)
+    tg = [t.cuda() for t in toks]
+    prev = D.CONV_PRECISION
+    try:
+        outs = {}
+        for prec in ("bf16x3", "bf16x3pre"):
+            D.CONV_PRECISION = prec
+            outs[prec] = m.depth_head(tg, images=imgs.cuda(), patch_start_idx=psi)
+    finally:
+        D.CONV_PRECISION = prev
+    assert torch.equal(outs["bf16x3"][0], outs["bf16x3pre"][0])
+    assert torch.equal(outs["bf16x3"][1], outs["bf16x3pre"][1])
+
+
 def test_alignment_head_bf16_tier(models):
     m, sd = models
     from aligned_vggt.utils.synthetic import synthetic_images

@@ -115,10 +115,19 @@ def _conv_call(N, prec, xr, n, hi, wi, ci, wp, b, co, k, s, p, y, **kw):
     if prec == "fp32":
         return N.conv2d_f32(xr, n, hi, wi, ci, wp, b, co, k, k, s, p, y, **kw)
     w_hi, w_lo = N.split_bf16x2(wp)
+    if prec == "bf16x3pre":
+        # pre-split activation (LDS-DMA gather): bitwise equal to the register-staged form
+        relu_in = kw.pop("relu_in", False)
+        x_hi, x_lo = N.split_act_bf16x2(xr, relu_in)
+        N.conv2d_bf16x3_pre(x_hi, x_lo, n, hi, wi, ci, w_hi, w_lo, b, co, k, k, s, p, y, **kw)
+        y2 = torch.empty_like(y)
+        N.conv2d_bf16x3(xr, n, hi, wi, ci, w_hi, w_lo, b, co, k, k, s, p, y2, relu_in=relu_in, **kw)
+        assert torch.equal(y, y2)
+        return y
     return N.conv2d_bf16x3(xr, n, hi, wi, ci, w_hi, w_lo, b, co, k, k, s, p, y, **kw)
 
 
-@pytest.mark.parametrize("prec,tol", [("fp32", 2e-6), ("bf16x3", 3e-5)])
+@pytest.mark.parametrize("prec,tol", [("fp32", 2e-6), ("bf16x3", 3e-5), ("bf16x3pre", 3e-5)])
 @pytest.mark.parametrize("case", ["3x3", "3x3s2", "1x1pos", "rcu", "shuffle4", "shuffle2", "co2", "co256", "co192"])
 def test_conv2d_f32(N, case, prec, tol):
     """fp32 implicit-GEMM conv (exact f32 MFMA) and its split-bf16 form
