@@ -1647,6 +1647,13 @@ int gemm_impl(const void* A, int64_t lda, const void* W, int64_t ldw, const floa
   if (g_vggt_gemm_tile < 0 && mode == 7 && (M >= 16384 || epi == VGGT_EPI_GELU_BF16) && N <= PP_MAXN &&
       (persist_policy() & 1))
     mode = 9;
+  // ... and the narrow (N = 1024) bf16 / f32-output GEMMs of the training
+  // recompute and backward (dX = dY W): 192-row persistent tiles instead of
+  // 128x128 at 22,000 rows: K = 4096 177 -> 144 us, K = 3072 132 -> 112 us,
+  // K = 1024 51.5 -> 45.4 us (gemmbench r3tr)
+  if (g_vggt_gemm_tile < 0 && mode == 0 && epi != VGGT_EPI_RESID_F32 && M >= 16384 && N % 256 == 0 &&
+      N <= PP_MAXN && K % PBK == 0 && (persist_policy() & 1))
+    mode = 9;
   // the LayerScale-residual fc2 (N = 1024, K = 4096) on 192-row persistent tiles:
   // 216 -> 201 us, aggregator step 104.0 -> 102.3 ms (same box, r3o); the
   // K = 1024 proj stays on the 128x128 form (76 vs 80 us)

@@ -46,7 +46,7 @@ def main():
     M = args.tokens
     x = (torch.rand(M, 4096, device=dev) * 2 - 1).bfloat16()
     shapes = {"qkv": (3072, 1024), "proj": (1024, 1024), "fc1": (4096, 1024), "fc2": (1024, 4096),
-              "fc1_k4096": (4096, 4096), "qkv_k4096": (3072, 4096),
+              "fc1_k4096": (4096, 4096), "qkv_k4096": (3072, 4096), "dx_k3072": (1024, 3072),
               "fc1_k64": (4096, 64), "fc1_k128": (4096, 128), "fc1_k256": (4096, 256), "fc2_k64": (1024, 64)}
     wq = (torch.randn(3072, 1024, device=dev) * 0.03).bfloat16()
     oq = torch.empty(M, 3072, device=dev, dtype=torch.bfloat16)
