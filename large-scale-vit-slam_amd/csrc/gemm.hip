@@ -47,6 +47,9 @@ struct Epi {
 };
 
 constexpr int EPI_QKNORM_D64 = 16, EPI_QKNORM_D128 = 17;  // internal epilogue ids
+// GELU that also stores the pre-activation (bf16 Linear output) into out2 for
+// the GELU backward (vggt_gemm_bf16_gelu_pre): the persistent form's id
+constexpr int EPI_GELU_PRE = 18;
 
 // bf16 GELU of the two bf16 values packed in d, from gelu_lut (global memory)
 // or its LDS copy (|x| in [2^-16, 2^6): positive half, then negative half).  Outside
@@ -1057,7 +1060,8 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
   static_assert(C::AL * 1024 * 8 == C::ABYTES, "whole DMA pieces per wave");
   constexpr int LPS = C::AL + C::WL;
   // buffer stores per wave per tile (RESID: the residual and its optional mirror)
-  constexpr int NST = EPI == VGGT_EPI_F32 ? C::NI * C::MI
+  constexpr bool GELU = EPI == VGGT_EPI_GELU_BF16 || EPI == EPI_GELU_PRE;
+  constexpr int NST = EPI == VGGT_EPI_F32 || EPI == EPI_GELU_PRE ? C::NI * C::MI
                       : EPI == VGGT_EPI_RESID_F32 ? 2 * C::NI * C::MI : C::NI * C::MI / 2;
   static_assert(LPS + NST <= 63, "vmcnt range");
   static_assert(EPI != VGGT_EPI_RESID_F32 || BMT == 192, "residual tiles are 192 rows (register budget)");
@@ -1079,7 +1083,7 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
   if constexpr (EPI == VGGT_EPI_RESID_F32)
     for (int i = threadIdx.x; i < N; i += PNT) gam_s[i] = ep.gamma[i];
   uint16_t* lut_s = (uint16_t*)(bias_s + N);  // GELU: the bf16 table
-  if constexpr (EPI == VGGT_EPI_GELU_BF16)
+  if constexpr (GELU)
     for (int i = threadIdx.x; i < GELU_LUT_N; i += PNT) ((uint32_t*)lut_s)[i] = ((const uint32_t*)gelu_lut)[i];
   // EPI_QKNORM_D64: q/k norm weights (qw qb kw kb, 64 each), RoPE-2D cos / sin
   // tables [tab_len][32] and the positions (y | x << 8 per position index)
@@ -1434,6 +1438,10 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
     } else {
       // after the swap, row group rg holds fragment ni + (rg & 1), features 8 * (rg >> 1) ..
       const int ncol = (rg & 1) * 16 + (rg >> 1) * 8;
+      const __amdgpu_buffer_rsrc_t rpre = __builtin_amdgcn_make_buffer_rsrc(
+          EPI == EPI_GELU_PRE ? (void*)((bf16_t*)(void*)ep.out2 + (int64_t)m0 * ep.ldo2) : ep.out, 0,
+          EPI == EPI_GELU_PRE ? (int)(min(M - m0, BMT) * ep.ldo2 * 2) : 0, 0x00020000);
+      (void)rpre;
 #pragma unroll
       for (int np = 0; np < C::NI; np += 2) {
         const f32x4 bv0 = *(const f32x4*)(bias_s + n0 + wn * C::WN + np * 16 + 4 * rg);
@@ -1445,7 +1453,14 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
           const f32x4 v0 = acc[np][mi] + bv0, v1 = acc[np + 1][mi] + bv1;
           uint32_t a0 = pack_bf2(v0[0], v0[1]), a1 = pack_bf2(v0[2], v0[3]);
           uint32_t b0 = pack_bf2(v1[0], v1[1]), b1 = pack_bf2(v1[2], v1[3]);
-          if constexpr (EPI == VGGT_EPI_GELU_BF16) {
+          if constexpr (EPI == EPI_GELU_PRE) {
+            // the pre-activation, same pairing and row as the activation store
+            const auto p0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+            const auto p1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+            const u32x4 pp = {p0[0], p1[0], p0[1], p1[1]};
+            __builtin_amdgcn_raw_buffer_store_b128(pp, rpre, (ml * (int)ep.ldo2 + nl) * 2, 0, 0);
+          }
+          if constexpr (GELU) {
             // GELU of the bf16 Linear output (autocast), from the LDS table of
             // torch's float32 GELU rounded to bf16 (gelu_lut.h)
             a0 = gelu2_lut(a0, lut_s);
@@ -1478,7 +1493,7 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
 inline int ppp_lds_bytes(int epi, int bmt, int N, const Epi& ep) {
   int64_t b = 2 * ((int64_t)bmt * PBK * 2 + 256 * PBK * 2) + (int64_t)N * 4;
   if (epi == VGGT_EPI_RESID_F32) b += (int64_t)N * 4;
-  if (epi == VGGT_EPI_GELU_BF16) b += (int64_t)GELU_LUT_N * 2 * 2;
+  if (epi == VGGT_EPI_GELU_BF16 || epi == EPI_GELU_PRE) b += (int64_t)GELU_LUT_N * 2 * 2;
   if (epi == EPI_QKNORM_D64) {
     b += 256 * 4;
     if (ep.rope_mode == VGGT_ROPE_2D) b += 2 * (int64_t)ep.tab_len * 32 * 4 + (((int64_t)ep.period * 2 + 15) & ~15);
@@ -1549,7 +1564,8 @@ int launch_ppp_bm(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, in
     const char* e = getenv("VGGT_GEMM_FULLK");
     return e ? atoi(e) : 5;
   }();
-  const int bit = EPI == EPI_QKNORM_D64 ? 2 : EPI == VGGT_EPI_RESID_F32 ? 4 : 1;
+  // (GELU + pre-activation keeps half-K segments: whole-K ones spill at 256 rows)
+  const int bit = EPI == EPI_QKNORM_D64 ? 2 : EPI == VGGT_EPI_RESID_F32 ? 4 : EPI == EPI_GELU_PRE ? 8 : 1;
   if (fk & bit) return launch_ppp_fk<EPI, BMT, true>(a, lda, w, ldw, M, N, K, ep, s);
   return launch_ppp_fk<EPI, BMT, false>(a, lda, w, ldw, M, N, K, ep, s);
 }
@@ -1665,14 +1681,17 @@ int gemm_impl(const void* A, int64_t lda, const void* W, int64_t ldw, const floa
   if (mode == 1 && N % 256) mode = 2;
   // per-lane 32-bit DMA offsets span one 256-row panel
   if (mode != 0 && (int64_t)RBM * (lda > ldw ? lda : ldw) * 2 >= (1ll << 31)) return VGGT_ERR_SHAPE;
-  if (mode == 9 && (N % 256 || N > PP_MAXN || K % PBK || (epi == VGGT_EPI_GELU_BF16 && out2) ||
+  if (mode == 9 && (N % 256 || N > PP_MAXN || K % PBK ||
                     (int64_t)PBM * (ldo > ldo2 ? ldo : ldo2) * 4 >= (1ll << 31)))
     mode = K % PBK ? 2 : epi == VGGT_EPI_RESID_F32 ? 0 : 7;  // the persistent form: N % 256 == 0, N <= 4096
   if (mode == 9) {
     int rc;
     switch (epi) {
       case VGGT_EPI_BF16: rc = launch_ppp<VGGT_EPI_BF16>(a, lda, w, ldw, M, N, K, ep, s); break;
-      case VGGT_EPI_GELU_BF16: rc = launch_ppp<VGGT_EPI_GELU_BF16>(a, lda, w, ldw, M, N, K, ep, s); break;
+      case VGGT_EPI_GELU_BF16:
+        rc = out2 ? launch_ppp<EPI_GELU_PRE>(a, lda, w, ldw, M, N, K, ep, s)
+                  : launch_ppp<VGGT_EPI_GELU_BF16>(a, lda, w, ldw, M, N, K, ep, s);
+        break;
       case VGGT_EPI_RESID_F32: rc = launch_ppp<VGGT_EPI_RESID_F32>(a, lda, w, ldw, M, N, K, ep, s); break;
       case VGGT_EPI_F32: rc = launch_ppp<VGGT_EPI_F32>(a, lda, w, ldw, M, N, K, ep, s); break;
       default: return VGGT_ERR_UNSUPPORTED;
