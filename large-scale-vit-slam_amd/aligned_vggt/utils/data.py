@@ -2,7 +2,7 @@
 from __future__ import annotations
 
 import random
-from typing import List
+from typing import Optional, List
 
 import torch
 import torch.nn.functional as F
@@ -50,15 +50,51 @@ def convertDictListsToTensors(chunked_dict: dict, overlap: int, out_dict: dict =
             out_dict[key] = torch.cat(chunked_dict[key], dim=1)
 
 
-def moveDictListItemToCPU(chunked_dict: dict, itemIndex: int) -> None:
-    """data.py:89-106."""
+def _to_host(t: torch.Tensor, pending: Optional[list]) -> torch.Tensor:
+    if pending is None or t.device.type != "cuda":
+        return t.cpu()
+    # pinned destination, copied on a side stream after everything queued so far:
+    # the next chunk's kernels do not wait for the PCIe transfer
+    dst = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    cur = torch.cuda.current_stream(t.device)
+    side = _side_stream(t.device)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        dst.copy_(t, non_blocking=True)
+    t.record_stream(side)  # the allocator keeps t's memory until the copy is done
+    ev = torch.cuda.Event()
+    ev.record(side)
+    pending.append(ev)
+    return dst
+
+
+_SIDE = {}
+
+
+def _side_stream(device) -> "torch.cuda.Stream":
+    s = _SIDE.get(device)
+    if s is None:
+        s = _SIDE[device] = torch.cuda.Stream(device)
+    return s
+
+
+def moveDictListItemToCPU(chunked_dict: dict, itemIndex: int, pending: Optional[list] = None) -> None:
+    """data.py:89-106.  ``pending`` (a list): the copies run asynchronously into
+    pinned host tensors and their completion events are appended -- the caller
+    must wait on them (``wait_host_copies``) before reading the host tensors."""
     for key in chunked_dict.keys():
         v = chunked_dict[key]
         if isinstance(v, list) and len(v) >= (abs(itemIndex) if itemIndex < 0 else itemIndex + 1):
             if isinstance(v[0], list):
-                v[itemIndex] = [(it.cpu() if isinstance(it, torch.Tensor) else it) for it in v[itemIndex]]
+                v[itemIndex] = [(_to_host(it, pending) if isinstance(it, torch.Tensor) else it) for it in v[itemIndex]]
             elif isinstance(v[itemIndex], torch.Tensor):
-                v[itemIndex] = v[itemIndex].cpu()
+                v[itemIndex] = _to_host(v[itemIndex], pending)
+
+
+def wait_host_copies(pending: list) -> None:
+    for ev in pending:
+        ev.synchronize()
+    pending.clear()
 
 
 def alignAndConvertOutputs(predictions: dict, batch: dict, chunked_batch: dict, alignment_type: str, seq_width: int,

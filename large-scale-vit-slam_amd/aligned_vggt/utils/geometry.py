@@ -35,8 +35,11 @@ def averagePoseEncodings(pose_encodings: torch.Tensor) -> torch.Tensor:
     q = q / q.norm(dim=-1, keepdim=True).clamp(min=1e-8)
     w = (torch.ones(B, Nn, device=q.device, dtype=q.dtype) / Nn).unsqueeze(-1).unsqueeze(-1)
     M = (w * (q.unsqueeze(-1) * q.unsqueeze(-2))).sum(dim=1)
-    _, vec = torch.linalg.eigh(M)
-    v = vec[..., -1]
+    # the (B, 4, 4) eigenproblem on the host: LAPACK, as the CPU oracle; the device
+    # solver's launches, workspace fills and host round trips left the GPU idle
+    # ~13 ms per chunk (profiles/r3h gap analysis); one tiny sync instead
+    _, vec = torch.linalg.eigh(M.cpu())
+    v = vec[..., -1].to(M.device)
     v = v / v.norm(dim=-1, keepdim=True)
     return torch.cat([avg_t, v.unsqueeze(1)], dim=-1).float()
 
