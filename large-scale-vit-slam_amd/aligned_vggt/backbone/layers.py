@@ -70,12 +70,16 @@ class Attention(nn.Module):
 # q/k norm + RoPE fused into the qkv GEMM epilogue (vggt_gemm_qkv); VGGT_FUSED_QKV=0
 # selects the separate headnorm_rope launch (A/B and fallback for odd shapes).
 _FUSED_QKV = os.environ.get("VGGT_FUSED_QKV", "1") != "0"
-# VGGT_FUSED_ADD_LN=1: fc2 as a plain GEMM + one fused residual-add /
-# next-LayerNorm row pass (vggt_resid_add_layernorm).  Off by default: in the
-# model (r2c, same box) plain fc2 226.6 us + the row pass 44.8 us - the saved
-# norm1 24.6 us = 246.8 us vs 235.2 us for the fp32 read-modify-write epilogue
-# of the 128x128 form (whose two workgroups per CU overlap the RMW).
-_FUSED_ADD_LN = os.environ.get("VGGT_FUSED_ADD_LN", "0") == "1"
+# VGGT_FUSED_ADD_LN bits: 1 = fc2 as a plain GEMM + one fused residual-add /
+# next-LayerNorm row pass (vggt_resid_add_layernorm) instead of the GEMM's fp32
+# read-modify-write epilogue + the next block's norm1; 2 = the same for proj
+# (+ norm2).  Default 3 since round 2: with the persistent GEMM the plain fc2 is
+# 146-150 vs 179-183 us (gemmbench: the RMW epilogue bursts on HBM after every
+# round of tiles), and the aggregator step went 103.4 -> 101.8 ms (bit 1, 3 x 2
+# same-box alternation, profiles/r4/ab_fused_add_ln.md), then 103.0 -> 102.5 ms
+# with bit 2 as well.  Round 1 (r2c) measured the opposite with the 128x128 fc2
+# form: 246.8 vs 235.2 us.
+_FUSED_ADD_LN = int(os.environ.get("VGGT_FUSED_ADD_LN", "3"))
 
 
 class RopeTables:
@@ -172,14 +176,21 @@ class Block(nn.Module):
         nb, rows, n = groups
         N.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], ao, nb, H, n, n, D, rows, rows, rows, tag=tag)
         w, b = pack_linear(self.attn.proj)
-        N.gemm_bf16(ao, w, b, xs, N.EPI_RESID_F32, gamma=self._gamma(self.ls1, C, x.device))
-        N.layernorm(xs, self.norm2.weight, self.norm2.bias, self.norm2.eps, xn)
+        if (_FUSED_ADD_LN & 2) and C in (256, 512, 1024, 2048) and isinstance(self.norm2, nn.LayerNorm):
+            # proj with a plain bf16 epilogue, then one row pass: x += ls1 * proj, xn = norm2(x)
+            pj = ws.buf("blk_pj", M, C, torch.bfloat16)
+            N.gemm_bf16(ao, w, b, pj, N.EPI_BF16)
+            N.resid_add_layernorm(xs, pj, self._gamma(self.ls1, C, x.device), None, self.norm2.weight,
+                                  self.norm2.bias, self.norm2.eps, xn)
+        else:
+            N.gemm_bf16(ao, w, b, xs, N.EPI_RESID_F32, gamma=self._gamma(self.ls1, C, x.device))
+            N.layernorm(xs, self.norm2.weight, self.norm2.bias, self.norm2.eps, xn)
         w, b = pack_linear(self.mlp.fc1)
         hid = ws.buf("blk_h", M, w.shape[0], torch.bfloat16)
         N.gemm_bf16(xn, w, b, hid, N.EPI_GELU_BF16)
         w, b = pack_linear(self.mlp.fc2)
         # the row pass has kernels for C / 256 in {1, 2, 4, 8} only (norm.hip)
-        if not (_FUSED_ADD_LN and C in (256, 512, 1024, 2048)):
+        if not ((_FUSED_ADD_LN & 1) and C in (256, 512, 1024, 2048)):
             N.gemm_bf16(hid, w, b, xs, N.EPI_RESID_F32, gamma=self._gamma(self.ls2, C, x.device), out2=out2)
             return False
         # fc2 with a plain bf16 epilogue, then ONE row pass for the LayerScale
