@@ -78,8 +78,12 @@ _FUSED_QKV = os.environ.get("VGGT_FUSED_QKV", "1") != "0"
 # round of tiles), and the aggregator step went 103.4 -> 101.8 ms (bit 1, 3 x 2
 # same-box alternation, profiles/r4/ab_fused_add_ln.md), then 103.0 -> 102.5 ms
 # with bit 2 as well.  Round 1 (r2c) measured the opposite with the 128x128 fc2
-# form: 246.8 vs 235.2 us.
+# form: 246.8 vs 235.2 us.  Only from _FUSED_ADD_LN_MIN_ROWS token rows: at the
+# 154x518 sequence chunk (6,592 rows, fc2 = 140 tiles, less than one round) the
+# sequence measured 1651 vs 1661 ms per 43 chunks (neutral to slightly worse),
+# the 518^2 chunk 138.9 -> 137.8 ms and configs[2] 695 -> 689 ms (profiles/r4).
 _FUSED_ADD_LN = int(os.environ.get("VGGT_FUSED_ADD_LN", "3"))
+_FUSED_ADD_LN_MIN_ROWS = 16384
 
 
 class RopeTables:
@@ -176,7 +180,8 @@ class Block(nn.Module):
         nb, rows, n = groups
         N.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], ao, nb, H, n, n, D, rows, rows, rows, tag=tag)
         w, b = pack_linear(self.attn.proj)
-        if (_FUSED_ADD_LN & 2) and C in (256, 512, 1024, 2048) and isinstance(self.norm2, nn.LayerNorm):
+        fal = _FUSED_ADD_LN if M >= _FUSED_ADD_LN_MIN_ROWS else 0
+        if (fal & 2) and C in (256, 512, 1024, 2048) and isinstance(self.norm2, nn.LayerNorm):
             # proj with a plain bf16 epilogue, then one row pass: x += ls1 * proj, xn = norm2(x)
             pj = ws.buf("blk_pj", M, C, torch.bfloat16)
             N.gemm_bf16(ao, w, b, pj, N.EPI_BF16)
@@ -190,7 +195,7 @@ class Block(nn.Module):
         N.gemm_bf16(xn, w, b, hid, N.EPI_GELU_BF16)
         w, b = pack_linear(self.mlp.fc2)
         # the row pass has kernels for C / 256 in {1, 2, 4, 8} only (norm.hip)
-        if not ((_FUSED_ADD_LN & 1) and C in (256, 512, 1024, 2048)):
+        if not ((fal & 1) and C in (256, 512, 1024, 2048)):
             N.gemm_bf16(hid, w, b, xs, N.EPI_RESID_F32, gamma=self._gamma(self.ls2, C, x.device), out2=out2)
             return False
         # fc2 with a plain bf16 epilogue, then ONE row pass for the LayerScale
