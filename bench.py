@@ -313,7 +313,10 @@ def bench_train(args, world, rank, dev):
     P = 5 + (H // 14) * (W // 14)
     head = AlignmentHead(in_dim=2048, num_memory_tokens=8).to(dev).train()
     synthetic_init_(head, seed=0)
-    opt = torch.optim.AdamW(head.parameters(), lr=5e-5, weight_decay=0.05)
+    # fused AdamW (one multi-tensor kernel per step instead of torch's foreach
+    # chain); VGGT_ADAMW_FUSED=0 selects the foreach implementation for A/B
+    fused = os.environ.get("VGGT_ADAMW_FUSED", "1") != "0"
+    opt = torch.optim.AdamW(head.parameters(), lr=5e-5, weight_decay=0.05, fused=fused)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     toks = [torch.randn(1, S, P, 2048, device=dev, generator=g) for _ in range(2)]
     wcs = torch.randn(1, 1, 8, device=dev, generator=g)
