@@ -27,6 +27,7 @@ parameter gradients are the bf16 GEMM results widened to fp32.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -107,13 +108,44 @@ class _LinBwd:
         N.gemm_bf16(a, b, _zeros(K, dy.device), out, N.EPI_F32)
 
 
-def _lin_grads(lin: nn.Linear, device):
-    return torch.zeros_like(lin.weight, dtype=torch.float32), (
-        torch.zeros_like(lin.bias, dtype=torch.float32) if lin.bias is not None else None)
+_ARENA = os.environ.get("VGGT_GRAD_ARENA", "1") != "0"
 
 
-def _ln_grads(ln: nn.LayerNorm):
-    return torch.zeros_like(ln.weight, dtype=torch.float32), torch.zeros_like(ln.bias, dtype=torch.float32)
+class _GradArena:
+    """The zero-initialised fp32 parameter gradients of one backward, carved out of
+    ONE zero-filled buffer: one fill launch instead of one per parameter (the
+    training step issued ~670 fills of ~4 us each, plus their dispatch gaps).
+    The views are contiguous and shaped like their parameters, so autograd's
+    AccumulateGrad adopts them as .grad without a copy."""
+
+    def __init__(self, device, tensors):
+        self.buf = torch.zeros(sum(t.numel() for t in tensors if t is not None), device=device) if _ARENA else None
+        self.off = 0
+
+    def like(self, t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+        if t is None:
+            return None
+        if self.buf is None:  # VGGT_GRAD_ARENA=0: one zero fill per parameter (A/B)
+            return torch.zeros_like(t, dtype=torch.float32)
+        v = self.buf[self.off:self.off + t.numel()].view(t.shape)
+        self.off += t.numel()
+        return v
+
+    def lin(self, lin: nn.Linear):
+        return self.like(lin.weight), self.like(lin.bias)
+
+    def ln(self, ln: nn.LayerNorm):
+        return self.like(ln.weight), self.like(ln.bias)
+
+
+def _params_of(*mods) -> list:
+    out = []
+    for m in mods:
+        if isinstance(m, torch.Tensor):
+            out.append(m)
+        elif isinstance(m, (nn.Linear, nn.LayerNorm)):
+            out += [m.weight, m.bias]
+    return out
 
 
 def _mlp_fwd(blk, x1: torch.Tensor, ws: Workspace, pfx: str):
@@ -210,18 +242,21 @@ class FrameBlockFn(torch.autograd.Function):
         nb, rows = groups
         t = FrameBlockFn._recompute(blk, x, groups, rope, ws)
         g = {}
-        g["norm1.w"], g["norm1.b"] = _ln_grads(blk.norm1)
-        g["qkv.w"], g["qkv.b"] = _lin_grads(blk.attn.qkv, x.device)
         qn, kn = blk.attn.q_norm, blk.attn.k_norm
+        ar = _GradArena(x.device, _params_of(blk.norm1, blk.attn.qkv, *((qn, kn) if t["has_norm"] else ()),
+                                             blk.attn.proj, blk.ls1.gamma, blk.norm2, blk.mlp.fc1, blk.mlp.fc2,
+                                             blk.ls2.gamma))
+        g["norm1.w"], g["norm1.b"] = ar.ln(blk.norm1)
+        g["qkv.w"], g["qkv.b"] = ar.lin(blk.attn.qkv)
         if t["has_norm"]:
-            g["qn.w"], g["qn.b"] = _ln_grads(qn)
-            g["kn.w"], g["kn.b"] = _ln_grads(kn)
-        g["proj.w"], g["proj.b"] = _lin_grads(blk.attn.proj, x.device)
-        g["ls1"] = torch.zeros_like(blk.ls1.gamma)
-        g["norm2.w"], g["norm2.b"] = _ln_grads(blk.norm2)
-        g["fc1.w"], g["fc1.b"] = _lin_grads(blk.mlp.fc1, x.device)
-        g["fc2.w"], g["fc2.b"] = _lin_grads(blk.mlp.fc2, x.device)
-        g["ls2"] = torch.zeros_like(blk.ls2.gamma)
+            g["qn.w"], g["qn.b"] = ar.ln(qn)
+            g["kn.w"], g["kn.b"] = ar.ln(kn)
+        g["proj.w"], g["proj.b"] = ar.lin(blk.attn.proj)
+        g["ls1"] = ar.like(blk.ls1.gamma)
+        g["norm2.w"], g["norm2.b"] = ar.ln(blk.norm2)
+        g["fc1.w"], g["fc1.b"] = ar.lin(blk.mlp.fc1)
+        g["fc2.w"], g["fc2.b"] = ar.lin(blk.mlp.fc2)
+        g["ls2"] = ar.like(blk.ls2.gamma)
         lb = _LinBwd(ws, M)
         dx = dout.float().contiguous().clone()
         _mlp_bwd(blk, dx, t["x1"], t["xn2"], t["hpre"], t["h"], t["br2"], g, lb, ws, "fbb_")
@@ -344,19 +379,22 @@ class TemporalBlockFn(torch.autograd.Function):
         t = TemporalBlockFn._recompute(blk, x, y, groups, nq, nk, rq, rk, ws)
         My = t["ysrc"].shape[0]
         g = {}
-        for nm in ("norm1", "norm3", "norm2"):
-            g[nm + ".w"], g[nm + ".b"] = _ln_grads(getattr(blk, nm))
-        for nm in ("q", "k", "v", "proj"):
-            g[nm + ".w"], g[nm + ".b"] = _lin_grads(getattr(blk.attn, nm), x.device)
         qn, kn = blk.attn.q_norm, blk.attn.k_norm
         has_norm = isinstance(qn, nn.LayerNorm)
+        ar = _GradArena(x.device, _params_of(blk.norm1, blk.norm3, blk.norm2, blk.attn.q, blk.attn.k, blk.attn.v,
+                                             blk.attn.proj, *((qn, kn) if has_norm else ()), blk.ls1.gamma,
+                                             blk.mlp.fc1, blk.mlp.fc2, blk.ls2.gamma))
+        for nm in ("norm1", "norm3", "norm2"):
+            g[nm + ".w"], g[nm + ".b"] = ar.ln(getattr(blk, nm))
+        for nm in ("q", "k", "v", "proj"):
+            g[nm + ".w"], g[nm + ".b"] = ar.lin(getattr(blk.attn, nm))
         if has_norm:
-            g["qn.w"], g["qn.b"] = _ln_grads(qn)
-            g["kn.w"], g["kn.b"] = _ln_grads(kn)
-        g["ls1"] = torch.zeros_like(blk.ls1.gamma)
-        g["fc1.w"], g["fc1.b"] = _lin_grads(blk.mlp.fc1, x.device)
-        g["fc2.w"], g["fc2.b"] = _lin_grads(blk.mlp.fc2, x.device)
-        g["ls2"] = torch.zeros_like(blk.ls2.gamma)
+            g["qn.w"], g["qn.b"] = ar.ln(qn)
+            g["kn.w"], g["kn.b"] = ar.ln(kn)
+        g["ls1"] = ar.like(blk.ls1.gamma)
+        g["fc1.w"], g["fc1.b"] = ar.lin(blk.mlp.fc1)
+        g["fc2.w"], g["fc2.b"] = ar.lin(blk.mlp.fc2)
+        g["ls2"] = ar.like(blk.ls2.gamma)
         lb = _LinBwd(ws, Mx)
         dx = dout.float().contiguous().clone()
         _mlp_bwd(blk, dx, t["x1"], t["xn2"], t["hpre"], t["h"], t["br2"], g, lb, ws, "tbb_")
@@ -469,11 +507,12 @@ class ProjectInFn(torch.autograd.Function):
         ws = Workspace.get(dev)
         P1, M_in = P + 1, B * S * P
         dx = dx.float().contiguous()
-        dtw, dtb = _ln_grads(head.token_norm)
+        ar = _GradArena(dev, _params_of(head.token_norm, head.project_in))
+        dtw, dtb = ar.ln(head.token_norm)
         dpr = ws.buf("pib_dpr", M_in, C, torch.bfloat16)
         N.layernorm_bwd(pr, head.token_norm.weight, head.token_norm.eps, dx, dpr, False, dtw, dtb, M=M_in, group=P,
                         x_gstride=P, x_off=0, y_gstride=P1, y_off=1)
-        dw, db = _lin_grads(head.project_in, dev)
+        dw, db = ar.lin(head.project_in)
         N.colsum(dpr, db)
         tin = ws.buf("pi_in", M_in, Cin, torch.bfloat16)
         N.cast_f32_bf16(ctx.tokens.reshape(M_in, Cin), tin)
@@ -526,12 +565,12 @@ class LinearF32Fn(torch.autograd.Function):
             dpre = dy2
         db = None
         if ctx.has_b:
-            db = torch.zeros(Nn, device=dy.device)
             if Nn % 4 == 0:
-                N.colsum(dpre, db)
+                db = torch.empty(Nn, device=dy.device)  # written, not accumulated
+                N.colsum(dpre, db, False)
             else:
                 db = dpre.sum(0)
-        dw = torch.zeros_like(w, dtype=torch.float32)
+        dw = torch.empty_like(w, dtype=torch.float32)  # vggt_wgrad_f32 without accumulate writes every element
         N.wgrad_f32(dpre, x2, dw, False)
         dx = None
         if ctx.needs_input_grad[0]:
@@ -561,8 +600,8 @@ class LayerNormF32Fn(torch.autograd.Function):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(x2.shape).float().contiguous()
         dx = torch.empty_like(x2)
-        dw = torch.zeros_like(w, dtype=torch.float32)
-        db = torch.zeros_like(w, dtype=torch.float32)
+        ar = _GradArena(dx.device, [w, w])  # the parameter sums accumulate into zeroed outputs
+        dw, db = ar.like(w), ar.like(w)
         N.layernorm_bwd(x2, w.detach(), ctx.eps, dy2, dx, False, dw, db)
         return dx.view(ctx.shape), dw, db, None
 
@@ -590,8 +629,9 @@ class HeadNormRopeF32Fn(torch.autograd.Function):
         t2, w = ctx.saved_tensors
         eps, H, D, mode, pos, tabs, has_b = ctx.args
         grad = dout.float().contiguous().clone()
-        dw = torch.zeros_like(w) if w is not None else None
-        db = torch.zeros_like(w) if (w is not None and has_b) else None
+        ar = _GradArena(grad.device, [w, w if has_b else None])
+        dw = ar.like(w)
+        db = ar.like(w) if has_b else None
         N.headnorm_rope_bwd(t2, grad, H, H, D, w.detach() if w is not None else None, None, eps, mode,
                             pos if mode else None, pos.numel() if mode else 1, tabs[0] if mode else None,
                             tabs[1] if mode else None, dw, db)
