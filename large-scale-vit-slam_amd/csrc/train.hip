@@ -11,6 +11,8 @@
 // workspace, and a finalize pass adds the chunks in index order.
 #include <math.h>
 
+#include <stdlib.h>
+
 #include "common.h"
 #include "mfma_frag.h"
 
@@ -700,6 +702,123 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const bf16_t* __restric
       }
 }
 
+// The same product with the token tiles staged by LDS-DMA (buffer_load ... lds)
+// into a 3-slot ring, two tiles ahead, counted waits: no register round trip,
+// so the L2 latency of tile t+2 hides behind tiles t and t+1 (the register-
+// staged form waits vmcnt(0) once per 8 MFMAs).  The padded [32][128 + 8] row
+// image is reproduced by the per-lane source offsets: LDS unit u (16 B) of a
+// tile is row u / 17, 16-B chunk u % 17 (chunk 16 = the pad: loads a duplicate
+// of chunk 15); 10 pieces of 64 units per operand tile (640 >= 544 units, the
+// surplus lands in the tile's padding).  Rows past the split read zeros through
+// the descriptor's range check.
+typedef int wg_i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void wg_dma16(wg_i32x4 rsrc, uint32_t voff, uint32_t soff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds)
+               : "memory");
+}
+__device__ __forceinline__ wg_i32x4 wg_rsrc(const void* base, uint32_t nbytes) {
+  const uint64_t b = (uint64_t)base;
+  wg_i32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  r[1] = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) & 0xffff;
+  r[2] = __builtin_amdgcn_readfirstlane(nbytes);
+  r[3] = 0x00020000;
+  return r;
+}
+
+constexpr int WG_TILE = 10 * 1024;       // LDS bytes per operand tile (10 DMA pieces)
+constexpr int WG_SLOT = 2 * WG_TILE;     // dY tile + X tile
+constexpr int WG_NSLOT = 3;
+
+__global__ __launch_bounds__(256) void wgrad_dma_kernel(const bf16_t* __restrict__ dy, int64_t ldy,
+                                                        const bf16_t* __restrict__ x, int64_t ldx, int M, int N,
+                                                        int K, int mchunk, float* __restrict__ part) {
+  using namespace vggt_frag;
+  static_assert(32 * Geo<128>::ROWP <= WG_TILE, "tile image fits its slot");
+  extern __shared__ __attribute__((aligned(16))) char wsm[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ntn = N / 128;
+  const int n0 = (blockIdx.x % ntn) * 128, k0 = (blockIdx.x / ntn) * 128;
+  const int mb = blockIdx.y * mchunk, me = min(M, mb + mchunk);
+  const int wn = (wave >> 1) * 64, wk = (wave & 1) * 64;
+  // descriptors over the split's rows only: rows past me read as zeros
+  const wg_i32x4 ry = wg_rsrc(dy + (int64_t)mb * ldy, (uint32_t)((me - mb) * ldy * 2));
+  const wg_i32x4 rx = wg_rsrc(x + (int64_t)mb * ldx, (uint32_t)((me - mb) * ldx * 2));
+  // waves 0-1 stage the dY tile, waves 2-3 the X tile, 5 pieces each:
+  // piece p = 5 (wave & 1) + i of operand wave >> 1
+  const bool xo = wave >= 2;
+  const wg_i32x4 rs = xo ? rx : ry;
+  const int64_t ld = xo ? ldx : ldy;
+  uint32_t voff[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int u = (5 * (wave & 1) + i) * 64 + lane;
+    const int r = min(u / 17, 31), c = min(u % 17, 15);
+    voff[i] = (uint32_t)(r * ld + (xo ? k0 : n0) + c * 8) * 2u;
+  }
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(wsm)) + (xo ? WG_TILE : 0) +
+                        5 * (wave & 1) * 1024;
+  const uint32_t st = __builtin_amdgcn_readfirstlane((uint32_t)(32 * ld * 2));
+  auto stage = [&](int slot, int t) {
+    const uint32_t b = lds0 + slot * WG_SLOT;
+    const uint32_t so = (uint32_t)t * st;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) wg_dma16(rs, voff[i], so, b + i * 1024);
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+  const int nt = (me - mb + 31) / 32;  // >= 1: the host never launches an empty split
+  stage(0, 0);
+  stage(1, 1);
+  asm volatile("s_waitcnt vmcnt(5)\n\ts_barrier" ::: "memory");  // tile 0 landed everywhere
+  int slot = 0;
+  for (int t = 0; t < nt; ++t) {
+    // tile t+2 into the slot tile t-1 used (every wave passed the barrier after it);
+    // past the split: zero reads into a slot nobody reads again
+    const int s2 = slot == 0 ? 2 : slot - 1;
+    stage(s2, t + 2);
+    const char* ty = wsm + slot * WG_SLOT;
+    const char* tx = ty + WG_TILE;
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        af[i] = trfrag<128>(ty, (wn >> 5) + i, 0, ss, lane);
+        bfr[i] = trfrag<128>(tx, (wk >> 5) + i, 0, ss, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    // tile t+1 landed (its 5 pieces are older than tile t+2's 5), reads of slot done
+    asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    slot = slot == 2 ? 0 : slot + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the surplus DMA before the workgroup ends
+  const int hl = lane >> 5;
+  float* pz = part + (int64_t)blockIdx.y * N * K;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = n0 + wn + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        const int k = k0 + wk + 32 * j + (lane & 31);
+        pz[(int64_t)n * K + k] = acc[i][j][r];
+      }
+}
+
 // out[n][k] (+)= round_bf16(sum_z part[z][n][k])  (fixed split order)
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int nz, int64_t nk,
                                                            float* __restrict__ out, int64_t ldo, int K,
@@ -973,8 +1092,25 @@ extern "C" int vggt_wgrad_bf16(const void* dy, int64_t ldy, const void* x, int64
   mchunk = (mchunk + 31) / 32 * 32;
   const int nz = (M + mchunk - 1) / mchunk;
   hipStream_t s = (hipStream_t)stream;
-  wgrad_bf16_kernel<<<dim3((N / 128) * (K / 128), nz), 256, 0, s>>>((const bf16_t*)dy, ldy, (const bf16_t*)x, ldx, M,
-                                                                    N, K, mchunk, (float*)ws);
+  // VGGT_WGRAD_DMA=0: the register-staged form (A/B)
+  static const bool use_dma = [] {
+    const char* e = getenv("VGGT_WGRAD_DMA");
+    return !(e && atoi(e) == 0);
+  }();
+  // LDS-DMA form: 32-bit descriptor ranges over one split
+  if (use_dma && (int64_t)mchunk * (ldy > ldx ? ldy : ldx) * 2 < (1ll << 31)) {
+    static bool attr = [] {
+      (void)hipFuncSetAttribute((const void*)wgrad_dma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                WG_NSLOT * WG_SLOT);
+      return true;
+    }();
+    (void)attr;
+    wgrad_dma_kernel<<<dim3((N / 128) * (K / 128), nz), 256, WG_NSLOT * WG_SLOT, s>>>(
+        (const bf16_t*)dy, ldy, (const bf16_t*)x, ldx, M, N, K, mchunk, (float*)ws);
+  } else {
+    wgrad_bf16_kernel<<<dim3((N / 128) * (K / 128), nz), 256, 0, s>>>((const bf16_t*)dy, ldy, (const bf16_t*)x, ldx,
+                                                                      M, N, K, mchunk, (float*)ws);
+  }
   const int64_t nk = (int64_t)N * K;
   wgrad_reduce_kernel<<<(unsigned)((nk + 255) / 256), 256, 0, s>>>((const float*)ws, nz, nk, dw, ldw, K, accumulate, 1);
   HIP_LAUNCH_CHECK();

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Time vggt_wgrad_bf16 at the alignment head's training shapes (22,000 tokens):
-fc1 / fc2 / qkv / proj weight gradients.  VGGT_WGRAD_TK selects the tile width."""
+fc1 / fc2 / qkv / proj weight gradients.  VGGT_WGRAD_DMA selects the staging (1 LDS-DMA, 0 registers)."""
 import os
 import sys
 
@@ -32,7 +32,7 @@ def main():
         us = a.elapsed_time(b) / 20 * 1e3
         ref = (dy.float().t() @ x.float())
         err = ((dw - ref).norm() / ref.norm()).item()
-        print(f"tk={os.environ.get('VGGT_WGRAD_TK', '256')} {name} {us:.1f} us {2 * M * Nn * K / us / 1e6:.0f} TF/s rel {err:.1e}",
+        print(f"dma={os.environ.get('VGGT_WGRAD_DMA', '1')} {name} {us:.1f} us {2 * M * Nn * K / us / 1e6:.0f} TF/s rel {err:.1e}",
               flush=True)
 
 
