@@ -28,6 +28,7 @@ points) stay on the rank that produced them unless ``gather_dense``.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -61,6 +62,27 @@ def apply_sequence_to_model(batch: dict, model, chunk_width, num_overlap, sample
     return predictions
 
 
+GROUP_TOKENS = 24576  # token rows per grouped encode (3 chunks of 16 x 154x518 frames)
+
+
+def _split_batch(enc: dict, B: int, n: int) -> List[dict]:
+    """Split an encode_chunk result over n chunks stacked along the batch
+    dimension (n * B) back into n per-chunk results (views)."""
+    outs: List[dict] = [{} for _ in range(n)]
+    for k, v in enc.items():
+        if torch.is_tensor(v) and v.dim() > 0 and v.shape[0] == n * B:
+            for c in range(n):
+                outs[c][k] = v[c * B:(c + 1) * B]
+        elif isinstance(v, (list, tuple)) and v and all(torch.is_tensor(t) and t.dim() > 0 and t.shape[0] == n * B
+                                                         for t in v):
+            for c in range(n):
+                outs[c][k] = [t[c * B:(c + 1) * B] for t in v]
+        else:
+            for c in range(n):
+                outs[c][k] = v
+    return outs
+
+
 def _overlap_of(S: int, num_overlap: int) -> int:
     """featureAligned_vggt.py:93."""
     return num_overlap if S > num_overlap else S - 1
@@ -72,13 +94,25 @@ class ChunkPipeline:
     ``encode_chunk(images)`` and ``align_chunk(enc, num_overlap, context)``
     (FeatureAlignedVGGT does) and be replicated on every rank."""
 
-    def __init__(self, model, group=None, device=None, gather_dense: bool = False):
+    def __init__(self, model, group=None, device=None, gather_dense: bool = False,
+                 encode_group: Optional[int] = None):
         self.model = model
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.device = device
         self.gather_dense = gather_dense
+        # encode_group: up to this many consecutive equal-length chunks encoded
+        # together as one batch (encode_chunk is context-free; every kernel on it
+        # is row- or (batch, head)-local), capped at GROUP_TOKENS token rows per
+        # encode.  Small chunks (154x518: 6,592 token rows, fc2 = 140 GEMM tiles
+        # on 256 CUs) fill the GPU poorly one at a time: configs[3] 1637 ->
+        # 1415-1466 ms per 43 chunks in groups of 3 (profiles/r4/encode_groups.md);
+        # 518^2 chunks (21,984 rows) stay single.  Single rank only: on W > 1 ranks
+        # an early encode would delay the baton.  VGGT_ENCODE_GROUP sets the default.
+        if encode_group is None:
+            encode_group = int(os.environ.get("VGGT_ENCODE_GROUP", "3"))
+        self.encode_group = max(1, encode_group) if self.world == 1 else 1
 
     # ----------------------------------------------------- frame transfer
     def _fetch(self, images: torch.Tensor, idx):
@@ -150,13 +184,33 @@ class ChunkPipeline:
         mine: Dict[int, dict] = {}
         local = None  # baton kept in memory when the next chunk stays on this rank (W == 1)
         my = list(range(r, n, W))
-        nxt = self._fetch(images, chunks[my[0]]) if my else None
+        # encode groups: runs of up to encode_group consecutive chunks of one length,
+        # at most GROUP_TOKENS token rows per encode
+        groups: List[List[int]] = []
+        for i in my:
+            cap = min(self.encode_group, max(1, GROUP_TOKENS // (B * len(chunks[i]) * max(P1 - 1, 1))))
+            if groups and len(groups[-1]) < cap and len(chunks[groups[-1][-1]]) == len(chunks[i]) \
+                    and groups[-1][-1] + W == i:
+                groups[-1].append(i)
+            else:
+                groups.append([i])
+        fetch = lambda g: [self._fetch(images, chunks[i]) for i in g]  # noqa: E731
+        nxt = fetch(groups[0]) if groups else None
+        encs: Dict[int, dict] = {}
+        gi = 0
         for j, i in enumerate(my):
-            # this chunk's frames (prefetched while the previous chunk ran), the
-            # next chunk's transfer queued behind them
-            x = self._ready(nxt)
-            nxt = self._fetch(images, chunks[my[j + 1]]) if j + 1 < len(my) else None
-            enc = self.model.encode_chunk(x)
+            if i not in encs:
+                # this group's frames (prefetched while the previous group ran), the
+                # next group's transfer queued behind them
+                xs = [self._ready(f) for f in nxt]
+                g = groups[gi]
+                gi += 1
+                nxt = fetch(groups[gi]) if gi < len(groups) else None
+                if len(g) == 1:
+                    encs[i] = self.model.encode_chunk(xs[0])
+                else:
+                    encs.update(zip(g, _split_batch(self.model.encode_chunk(torch.cat(xs, 0)), B, len(g))))
+            enc = encs.pop(i)
             ctx = None
             if i > 0:
                 Sp = len(chunks[i - 1])

@@ -123,3 +123,16 @@ def test_pipeline_single_rank_matches_sequential_loop():
                                                                           memory_shape=(2, NMEM, DEC))
     for k in ("pose_enc", "chunk_sim3_alignment_enc", "frame_se3_alignment_enc", "depth"):
         torch.testing.assert_close(got[k], ref[k], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("group", [1, 2, 3, 5])
+def test_pipeline_encode_groups_match_sequential_loop(group):
+    """Grouped encode (consecutive equal-length chunks batched through
+    encode_chunk) incl. a shorter tail chunk: bitwise equal to the loop."""
+    ref = _sequential(23, 6, 2)
+    g = torch.Generator().manual_seed(0)
+    images = torch.rand(2, 23, 3, 4, 5, generator=g)
+    got = ChunkPipeline(ToyAlignModel(), device=torch.device("cpu"), gather_dense=True, encode_group=group).run(
+        images, 6, 2, token_dims=(P1, C), memory_shape=(2, NMEM, DEC))
+    for k in ("pose_enc", "chunk_sim3_alignment_enc", "frame_se3_alignment_enc", "depth", "depth_conf"):
+        torch.testing.assert_close(got[k], ref[k], rtol=0, atol=0)

@@ -258,3 +258,27 @@ def test_feature_aligned_batch2(models):
     for key in ("pose_enc", "depth"):
         for x2, xa, xb in zip(ctx2[key], ctxa[key], ctxb[key]):
             assert _rel(x2[:1], xa) < 1e-5 and _rel(x2[1:], xb) < 1e-5, key
+
+
+@pytest.mark.parametrize("H,W", [(42, 56), (70, 56)])
+def test_pipeline_grouped_encode_matches(models, H, W):
+    """ChunkPipeline's grouped encode (consecutive equal-length chunks through
+    the aggregator / camera / depth heads as one batch) against one chunk at a
+    time, incl. a shorter tail chunk that stays ungrouped: every kernel on the
+    encode path is row- or (batch, head)-local, so the merged poses, Sim(3) /
+    SE(3) encodings and depths must agree to fp32 round-off."""
+    m, _ = models
+    from aligned_vggt.dist.pipeline import ChunkPipeline
+    from aligned_vggt.utils.synthetic import synthetic_images
+    N, w, ov = 14, 4, 1  # four chunks of 4 + a shorter tail chunk
+    imgs = synthetic_images(1, N, H, W, seed=21).cuda()
+    P1 = 6 + (H // 14) * (W // 14)
+    outs = {}
+    for g in (1, 2, 3):
+        outs[g] = ChunkPipeline(m, device=torch.device("cuda"), gather_dense=True, encode_group=g).run(
+            imgs, w, ov, token_dims=(P1, 1024), memory_shape=(1, 8, 512))
+    for g in (2, 3):
+        for k in ("pose_enc", "chunk_sim3_alignment_enc", "frame_se3_alignment_enc", "depth"):
+            e = _rel(outs[g][k], outs[1][k])
+            assert outs[g][k].shape == outs[1][k].shape, k
+            assert e < 1e-5, (g, k, e)
