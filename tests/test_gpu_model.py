@@ -277,7 +277,10 @@ def test_pipeline_grouped_encode_matches(models, H, W):
     for g in (1, 2, 3):
         outs[g] = ChunkPipeline(m, device=torch.device("cuda"), gather_dense=True, encode_group=g).run(
             imgs, w, ov, token_dims=(P1, 1024), memory_shape=(1, 8, 512))
-    for g in (2, 3):
+    # host-resident frames: grouped chunks arrive through the pinned side-stream prefetch
+    outs["host"] = ChunkPipeline(m, device=torch.device("cuda"), gather_dense=True, encode_group=3).run(
+        imgs.cpu(), w, ov, token_dims=(P1, 1024), memory_shape=(1, 8, 512))
+    for g in (2, 3, "host"):
         for k in ("pose_enc", "chunk_sim3_alignment_enc", "frame_se3_alignment_enc", "depth"):
             e = _rel(outs[g][k], outs[1][k])
             assert outs[g][k].shape == outs[1][k].shape, k
