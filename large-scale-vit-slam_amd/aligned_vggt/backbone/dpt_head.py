@@ -281,6 +281,15 @@ class DPTHead(nn.Module):
         B, S, _, H, W = images.shape
         if images.device.type != "cuda":
             raise RuntimeError("DPTHead: the MI355X hot path runs on HIP devices only (no CPU fallback)")
+        if B > 1 and B * S * H * W * 128 * 2 >= (1 << 31):
+            # a batch of chunks (ChunkPipeline's grouped encode) whose widest
+            # activation (128 channels at full resolution, bf16 halves) would pass
+            # the convolutions' 32-bit offsets: one chunk at a time (per-frame
+            # arithmetic, identical results)
+            outs = [self.forward([t[b:b + 1] for t in aggregated_tokens_list], images[b:b + 1], patch_start_idx,
+                                 frames_chunk_size, _scale[b:b + 1] if _scale is not None else None)
+                    for b in range(B)]
+            return torch.cat([o[0] for o in outs], 0), torch.cat([o[1] for o in outs], 0)
         dev = images.device
         ph, pw = H // self.patch_size, W // self.patch_size
         F_ = B * S

@@ -62,7 +62,10 @@ def apply_sequence_to_model(batch: dict, model, chunk_width, num_overlap, sample
     return predictions
 
 
-GROUP_TOKENS = 24576  # token rows per grouped encode (3 chunks of 16 x 154x518 frames)
+# token rows per grouped encode (VGGT_GROUP_TOKENS for A/B): 2 chunks of 16 x 518^2
+# frames (configs[2] 683 -> 644 ms per 5 chunks, profiles/r4/encode_groups.md) or
+# encode_group (3) chunks of 16 x 154x518
+GROUP_TOKENS = int(os.environ.get("VGGT_GROUP_TOKENS", "49152"))
 
 
 def _split_batch(enc: dict, B: int, n: int) -> List[dict]:
@@ -107,9 +110,10 @@ class ChunkPipeline:
         # is row- or (batch, head)-local), capped at GROUP_TOKENS token rows per
         # encode.  Small chunks (154x518: 6,592 token rows, fc2 = 140 GEMM tiles
         # on 256 CUs) fill the GPU poorly one at a time: configs[3] 1637 ->
-        # 1415-1466 ms per 43 chunks in groups of 3 (profiles/r4/encode_groups.md);
-        # 518^2 chunks (21,984 rows) stay single.  Single rank only: on W > 1 ranks
-        # an early encode would delay the baton.  VGGT_ENCODE_GROUP sets the default.
+        # 1415-1466 ms per 43 chunks in groups of 3; 518^2 chunks in pairs: the
+        # GEMM / attention rounds quantise better (profiles/r4/encode_groups.md).
+        # Single rank only: on W > 1 ranks an early encode would delay the baton.
+        # VGGT_ENCODE_GROUP sets the default.
         if encode_group is None:
             encode_group = int(os.environ.get("VGGT_ENCODE_GROUP", "3"))
         self.encode_group = max(1, encode_group) if self.world == 1 else 1
@@ -130,8 +134,12 @@ class ChunkPipeline:
         side = self.__dict__.get("_side")
         if side is None:
             side = self._side = torch.cuda.Stream(dev)
-        xd = torch.empty(xp.shape, dtype=xp.dtype, device=dev)
+        # allocated on the side stream (the copy's producer): a block allocated on
+        # the compute stream could be one whose previous contents queued compute
+        # kernels still read, and the side-stream copy is not ordered after them;
+        # _ready's record_stream covers the consumer side
         with torch.cuda.stream(side):
+            xd = torch.empty(xp.shape, dtype=xp.dtype, device=dev)
             xd.copy_(xp, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(side)

@@ -260,17 +260,18 @@ def test_feature_aligned_batch2(models):
             assert _rel(x2[:1], xa) < 1e-5 and _rel(x2[1:], xb) < 1e-5, key
 
 
-@pytest.mark.parametrize("H,W", [(42, 56), (70, 56)])
-def test_pipeline_grouped_encode_matches(models, H, W):
+@pytest.mark.parametrize("H,W,N,w,ov", [(42, 56, 14, 4, 1), (70, 56, 14, 4, 1), (518, 518, 28, 16, 4)])
+def test_pipeline_grouped_encode_matches(models, H, W, N, w, ov):
     """ChunkPipeline's grouped encode (consecutive equal-length chunks through
     the aggregator / camera / depth heads as one batch) against one chunk at a
     time, incl. a shorter tail chunk that stays ungrouped: every kernel on the
     encode path is row- or (batch, head)-local, so the merged poses, Sim(3) /
-    SE(3) encodings and depths must agree to fp32 round-off."""
+    SE(3) encodings and depths must agree to fp32 round-off.  At 518^2 two
+    16-frame chunks form one encode and the DPT head runs per chunk (its
+    32-bit offset guard)."""
     m, _ = models
     from aligned_vggt.dist.pipeline import ChunkPipeline
     from aligned_vggt.utils.synthetic import synthetic_images
-    N, w, ov = 14, 4, 1  # four chunks of 4 + a shorter tail chunk
     imgs = synthetic_images(1, N, H, W, seed=21).cuda()
     P1 = 6 + (H // 14) * (W // 14)
     outs = {}
