@@ -51,10 +51,29 @@ def apply_sequence_to_model(batch: dict, model, chunk_width, num_overlap, sample
     chunked = chunk_batch(batch, indices)
     predictions = None
     pending: list = []  # host copies in flight (pinned, side stream), waited for before the merge
+    # forward == align_chunk(encode_chunk(.)) (featureAligned_vggt.py): consecutive
+    # equal-length chunks share one encode, as in ChunkPipeline (same results)
+    grouped = hasattr(model, "encode_chunk") and hasattr(model, "align_chunk") and torch.is_tensor(batch["images"]) \
+        and batch["images"].is_cuda
+    groups = _encode_groups([len(c) for c in indices], batch["images"], model) if grouped else []
+    encs: dict = {}
+    gi = 0
     for i in range(len(indices)):
         gt = chunked["extrinsics"][i] if sample_mode in ("chunk_gt", "two_chunks") else None
         with torch.no_grad():
-            predictions = model(chunked["images"][i], num_overlap, predictions, gt_poses=gt)
+            if not grouped:
+                predictions = model(chunked["images"][i], num_overlap, predictions, gt_poses=gt)
+            else:
+                if i not in encs:
+                    g = groups[gi]
+                    gi += 1
+                    if len(g) == 1:
+                        encs[i] = model.encode_chunk(chunked["images"][i])
+                    else:
+                        B = chunked["images"][i].shape[0]
+                        xs = torch.cat([chunked["images"][j] for j in g], 0)
+                        encs.update(zip(g, _split_batch(model.encode_chunk(xs), B, len(g))))
+                predictions = model.align_chunk(encs.pop(i), num_overlap, predictions, gt_poses=gt)
         moveDictListItemToCPU(predictions, -2, pending)
     moveDictListItemToCPU(predictions, -1, pending)
     wait_host_copies(pending)
@@ -66,6 +85,26 @@ def apply_sequence_to_model(batch: dict, model, chunk_width, num_overlap, sample
 # frames (configs[2] 683 -> 644 ms per 5 chunks, profiles/r4/encode_groups.md) or
 # encode_group (3) chunks of 16 x 154x518
 GROUP_TOKENS = int(os.environ.get("VGGT_GROUP_TOKENS", "49152"))
+
+
+def _encode_groups(lengths: List[int], images: torch.Tensor, model, encode_group: Optional[int] = None
+                   ) -> List[List[int]]:
+    """Runs of consecutive equal-length chunks encoded together (at most
+    encode_group chunks and GROUP_TOKENS token rows per encode)."""
+    if encode_group is None:
+        encode_group = int(os.environ.get("VGGT_ENCODE_GROUP", "3"))
+    B, H, W = images.shape[0], images.shape[-2], images.shape[-1]
+    ps = getattr(getattr(model, "aggregator", None), "patch_size", 14)
+    ps = ps[0] if isinstance(ps, (tuple, list)) else int(ps)
+    P = (H // ps) * (W // ps) + 5
+    groups: List[List[int]] = []
+    for i, n in enumerate(lengths):
+        cap = min(max(1, encode_group), max(1, GROUP_TOKENS // (B * n * P)))
+        if groups and len(groups[-1]) < cap and lengths[groups[-1][-1]] == n:
+            groups[-1].append(i)
+        else:
+            groups.append([i])
+    return groups
 
 
 def _split_batch(enc: dict, B: int, n: int) -> List[dict]:
