@@ -231,16 +231,9 @@ class ChunkPipeline:
         mine: Dict[int, dict] = {}
         local = None  # baton kept in memory when the next chunk stays on this rank (W == 1)
         my = list(range(r, n, W))
-        # encode groups: runs of up to encode_group consecutive chunks of one length,
-        # at most GROUP_TOKENS token rows per encode
-        groups: List[List[int]] = []
-        for i in my:
-            cap = min(self.encode_group, max(1, GROUP_TOKENS // (B * len(chunks[i]) * max(P1 - 1, 1))))
-            if groups and len(groups[-1]) < cap and len(chunks[groups[-1][-1]]) == len(chunks[i]) \
-                    and groups[-1][-1] + W == i:
-                groups[-1].append(i)
-            else:
-                groups.append([i])
+        # encode groups (one rank: every chunk is ours, in order)
+        groups = (_encode_groups([len(c) for c in chunks], images, self.model, self.encode_group)
+                  if W == 1 else [[i] for i in my])
         fetch = lambda g: [self._fetch(images, chunks[i]) for i in g]  # noqa: E731
         nxt = fetch(groups[0]) if groups else None
         encs: Dict[int, dict] = {}
