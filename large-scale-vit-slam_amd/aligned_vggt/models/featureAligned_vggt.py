@@ -10,6 +10,8 @@ composition of featureAligned_vggt.py:96-143 is small per-frame device glue.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -24,6 +26,9 @@ from ..heads.alignment_head import AlignmentHead
 from ..utils.data import extri_to_pose_encoding, pose_encoding_to_extri
 from ..utils.geometry import averagePoseEncodings, closed_form_inverse_se3
 from ..utils.pose_enc import extri_intri_to_pose_encoding, pose_encoding_to_extri_intri
+
+# no-grad inference runs the per-chunk pose algebra on the host (see _align_chunk)
+_HOST_POSE = os.environ.get("VGGT_HOST_POSE", "1") != "0"
 
 try:  # optional, as in the reference (featureAligned_vggt.py:3); only used for from_pretrained
     from huggingface_hub import PyTorchModelHubMixin
@@ -122,20 +127,27 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
         chunk_sim3_enc, frame_se3_enc, memory_tokens, overlap_tokens = self.alignment_head(
             toks[-1], (H, W), overlap, overlap_tokens=ctx_overlap, memory_tokens=ctx_memory)
 
-        chunk_se3 = pose_encoding_to_extri(chunk_sim3_enc)
-        chunk_scale = chunk_sim3_enc[..., -1]
-        per_frame_se3 = torch.matmul(pose_encoding_to_extri(frame_se3_enc), chunk_se3)
+        dev = images.device
+        chunk_scale = chunk_sim3_enc[..., -1]  # on the device: depth / point scaling
+        # No-grad inference: the (B, S, 4, 4) quaternion / SE(3) algebra below runs on
+        # the host -- ~300 tiny elementwise launches per chunk on the device
+        # (profiles/r4w/align_chunk_ops.txt), and the Markley average already syncs
+        # on the host.  Same fp32 arithmetic; VGGT_HOST_POSE=0 keeps it on the device.
+        adev = torch.device("cpu") if (not train and _HOST_POSE and dev.type == "cuda") else dev
+        cs_a = chunk_sim3_enc.to(adev)
+        chunk_se3 = pose_encoding_to_extri(cs_a)
+        per_frame_se3 = torch.matmul(pose_encoding_to_extri(frame_se3_enc.to(adev)), chunk_se3)
         per_frame_se3 = torch.cat([chunk_se3, per_frame_se3], dim=1)
 
         point_identity_alignment = None
         if self.camera_head is not None:
-            extr, intr = pose_encoding_to_extri_intri(enc["cam_pose_enc"], image_size_hw=images.shape[-2:])
+            extr, intr = pose_encoding_to_extri_intri(enc["cam_pose_enc"].to(adev), image_size_hw=images.shape[-2:])
             extr = F.pad(extr, (0, 0, 0, 1, 0, 0, 0, 0), mode="constant")
             extr[:, :, 3, 3] = 1.0
             ident = closed_form_inverse_se3(extr[:, 0])
             point_identity_alignment = extr[:, 0].detach().clone()
             extr = extr @ ident.view(B, 1, 4, 4)
-            extr[:, :, :3, 3] *= chunk_scale.view(B, 1, 1)
+            extr[:, :, :3, 3] *= cs_a[..., -1].view(B, 1, 1)
             if context is not None:
                 if gt_poses is not None:
                     mean_camera_transform = gt_poses[:, :1].to(extr)
@@ -149,11 +161,13 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
                     else:
                         mean_camera_transform = ct
             else:
-                mean_camera_transform = torch.eye(4, device=images.device, dtype=images.dtype).view(1, 1, 4, 4).expand(
+                mean_camera_transform = torch.eye(4, device=adev, dtype=images.dtype).view(1, 1, 4, 4).expand(
                     B, -1, -1, -1)
             per_frame_se3 = torch.matmul(per_frame_se3, mean_camera_transform)
             aligned_extr = torch.matmul(extr, per_frame_se3)
             aligned_pose_enc = extri_intri_to_pose_encoding(aligned_extr, intr, image_size_hw=images.shape[-2:])
+            if adev != dev:
+                aligned_pose_enc = aligned_pose_enc.to(dev)
 
             predictions["overlap_tokens"] = overlap_tokens
             if context is None:
@@ -190,6 +204,10 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
 
         if self.point_head is not None:
             pts3d, pts3d_conf = enc["points"], enc["points_conf"]
+            if adev != dev:
+                per_frame_se3 = per_frame_se3.to(dev)
+                if point_identity_alignment is not None:
+                    point_identity_alignment = point_identity_alignment.to(dev)
             if self.camera_head is not None:
                 if context is not None:
                     pt = closed_form_inverse_se3(per_frame_se3[:, 0]).unsqueeze(1)
