@@ -102,6 +102,11 @@ def _scratch(in_shape, out_shape) -> nn.Module:
 # (exact f32 MFMA).
 CONV_PRECISION = os.environ.get("VGGT_CONV", "bf16x3pre")
 
+# The convolutions address their operands with 32-bit byte offsets
+# (conv.hip: VGGT_ERR_SHAPE at 2 GiB); a forward whose widest map reaches this
+# runs in groups of frames.  Module-level so tests can lower it.
+MAP_BYTES_LIMIT = 1 << 31
+
 
 def _pre() -> bool:
     return CONV_PRECISION == "bf16x3pre"
@@ -281,15 +286,29 @@ class DPTHead(nn.Module):
         B, S, _, H, W = images.shape
         if images.device.type != "cuda":
             raise RuntimeError("DPTHead: the MI355X hot path runs on HIP devices only (no CPU fallback)")
-        if B > 1 and B * S * H * W * 128 * 2 >= (1 << 31):
-            # a batch of chunks (ChunkPipeline's grouped encode) whose widest
-            # activation (128 channels at full resolution, bf16 halves) would pass
-            # the convolutions' 32-bit offsets: one chunk at a time (per-frame
-            # arithmetic, identical results)
-            outs = [self.forward([t[b:b + 1] for t in aggregated_tokens_list], images[b:b + 1], patch_start_idx,
-                                 frames_chunk_size, _scale[b:b + 1] if _scale is not None else None)
-                    for b in range(B)]
-            return torch.cat([o[0] for o in outs], 0), torch.cat([o[1] for o in outs], 0)
+        per_frame = H * W * 128 * 2  # widest activation: 128 channels at full resolution, bf16 halves
+        if B * S > 1 and B * S * per_frame >= MAP_BYTES_LIMIT:
+            # the widest map would pass the convolutions' 32-bit offsets (a long
+            # chunk, or a batch of chunks from ChunkPipeline's grouped encode):
+            # groups of frames instead -- every DPT op is per frame, so the
+            # results are identical (the reference itself runs frames_chunk_size
+            # frames at a time)
+            fpg = max(1, (MAP_BYTES_LIMIT - 1) // per_frame)
+            tl = [t.reshape(1, B * S, *t.shape[2:]) for t in aggregated_tokens_list]
+            im = images.reshape(1, B * S, *images.shape[2:])
+            fs = _scale.float().reshape(B, 1).expand(B, S).reshape(1, B * S) if _scale is not None else None
+            outs = [self._forward_frames([t[:, f0:f0 + fpg] for t in tl], im[:, f0:f0 + fpg], patch_start_idx,
+                                         fs[:, f0:f0 + fpg] if fs is not None else None)
+                    for f0 in range(0, B * S, fpg)]
+            preds = torch.cat([o[0] for o in outs], 1)
+            conf = torch.cat([o[1] for o in outs], 1)
+            return preds.view(B, S, *preds.shape[2:]), conf.view(B, S, *conf.shape[2:])
+        return self._forward_frames(aggregated_tokens_list, images, patch_start_idx, _scale)
+
+    def _forward_frames(self, aggregated_tokens_list: List[torch.Tensor], images: torch.Tensor, patch_start_idx: int,
+                        _scale: Optional[torch.Tensor]):
+        """``_scale``: (B,) per chunk or (B, S) per frame."""
+        B, S, _, H, W = images.shape
         dev = images.device
         ph, pw = H // self.patch_size, W // self.patch_size
         F_ = B * S
@@ -331,6 +350,6 @@ class DPTHead(nn.Module):
         npix = F_ * Ho * Wo
         preds = torch.empty(B, S, Ho, Wo, ncl - 1, device=dev)
         conf = torch.empty(B, S, Ho, Wo, device=dev)
-        scale = _scale.float().reshape(B, 1).expand(B, S).contiguous().view(-1) if _scale is not None else None
+        scale = _scale.float().reshape(B, -1).expand(B, S).contiguous().view(-1) if _scale is not None else None
         N.dpt_activate(out.t, npix, Ho * Wo, ncl, 0 if self.activation == "exp" else 1, scale, preds, conf)
         return preds, conf

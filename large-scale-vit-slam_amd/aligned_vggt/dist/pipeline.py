@@ -52,10 +52,14 @@ def apply_sequence_to_model(batch: dict, model, chunk_width, num_overlap, sample
     predictions = None
     pending: list = []  # host copies in flight (pinned, side stream), waited for before the merge
     # forward == align_chunk(encode_chunk(.)) (featureAligned_vggt.py): consecutive
-    # equal-length chunks share one encode, as in ChunkPipeline (same results)
-    grouped = hasattr(model, "encode_chunk") and hasattr(model, "align_chunk") and torch.is_tensor(batch["images"]) \
-        and batch["images"].is_cuda
-    groups = _encode_groups([len(c) for c in indices], batch["images"], model) if grouped else []
+    # equal-length chunks share one encode, as in ChunkPipeline (same results);
+    # VGGT_ENCODE_GROUP=1 keeps the reference's plain per-chunk model(...) call
+    encode_group = int(os.environ.get("VGGT_ENCODE_GROUP", "3"))
+    grouped = encode_group > 1 and hasattr(model, "encode_chunk") and hasattr(model, "align_chunk") \
+        and torch.is_tensor(batch["images"]) and batch["images"].is_cuda
+    if grouped and hasattr(model, "_check_frozen") and model.alignment_head.trainable():
+        model._check_frozen()  # forward()'s guard, which this path bypasses
+    groups = _encode_groups([len(c) for c in indices], batch["images"], model, encode_group) if grouped else []
     encs: dict = {}
     gi = 0
     for i in range(len(indices)):
@@ -94,9 +98,10 @@ def _encode_groups(lengths: List[int], images: torch.Tensor, model, encode_group
     if encode_group is None:
         encode_group = int(os.environ.get("VGGT_ENCODE_GROUP", "3"))
     B, H, W = images.shape[0], images.shape[-2], images.shape[-1]
-    ps = getattr(getattr(model, "aggregator", None), "patch_size", 14)
+    agg = getattr(model, "aggregator", None)
+    ps = getattr(agg, "patch_size", 14)
     ps = ps[0] if isinstance(ps, (tuple, list)) else int(ps)
-    P = (H // ps) * (W // ps) + 5
+    P = (H // ps) * (W // ps) + int(getattr(agg, "patch_start_idx", 5))  # + camera and register tokens
     groups: List[List[int]] = []
     for i, n in enumerate(lengths):
         cap = min(max(1, encode_group), max(1, GROUP_TOKENS // (B * n * P)))

@@ -710,7 +710,7 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const bf16_t* __restric
 // tile is row u / 17, 16-B chunk u % 17 (chunk 16 = the pad: loads a duplicate
 // of chunk 15); 10 pieces of 64 units per operand tile (640 >= 544 units, the
 // surplus lands in the tile's padding).  Rows past the split read zeros through
-// the descriptor's range check.
+// the per-tile descriptor's range check (see stage()).
 typedef int wg_i32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void wg_dma16(wg_i32x4 rsrc, uint32_t voff, uint32_t soff, uint32_t lds) {
   uint32_t keep;
@@ -746,14 +746,12 @@ __global__ __launch_bounds__(256) void wgrad_dma_kernel(const bf16_t* __restrict
   const int n0 = (blockIdx.x % ntn) * 128, k0 = (blockIdx.x / ntn) * 128;
   const int mb = blockIdx.y * mchunk, me = min(M, mb + mchunk);
   const int wn = (wave >> 1) * 64, wk = (wave & 1) * 64;
-  // descriptors over the split's rows only: rows past me read as zeros
-  const wg_i32x4 ry = wg_rsrc(dy + (int64_t)mb * ldy, (uint32_t)((me - mb) * ldy * 2));
-  const wg_i32x4 rx = wg_rsrc(x + (int64_t)mb * ldx, (uint32_t)((me - mb) * ldx * 2));
   // waves 0-1 stage the dY tile, waves 2-3 the X tile, 5 pieces each:
   // piece p = 5 (wave & 1) + i of operand wave >> 1
   const bool xo = wave >= 2;
-  const wg_i32x4 rs = xo ? rx : ry;
   const int64_t ld = xo ? ldx : ldy;
+  const bf16_t* src0 = xo ? x + (int64_t)mb * ldx : dy + (int64_t)mb * ldy;
+  const int rows = me - mb;
   uint32_t voff[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
@@ -763,12 +761,18 @@ __global__ __launch_bounds__(256) void wgrad_dma_kernel(const bf16_t* __restrict
   }
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(wsm)) + (xo ? WG_TILE : 0) +
                         5 * (wave & 1) * 1024;
-  const uint32_t st = __builtin_amdgcn_readfirstlane((uint32_t)(32 * ld * 2));
+  // The buffer range check sees voffset (+ inst offset) only, never soffset, so
+  // the descriptor is re-based per tile: base = row 32 t of the split, range =
+  // the split's remaining rows.  Rows past the split (the ragged last tile, and
+  // the surplus tiles t >= nt staged by the two-ahead prefetch) read zeros and
+  // touch no memory; every tile still issues its 5 pieces, so the counted waits
+  // below stay exact.
   auto stage = [&](int slot, int t) {
     const uint32_t b = lds0 + slot * WG_SLOT;
-    const uint32_t so = (uint32_t)t * st;
+    const int rem = max(0, rows - 32 * t);
+    const wg_i32x4 rs = wg_rsrc(src0 + (int64_t)32 * t * ld, (uint32_t)((int64_t)rem * ld * 2));
 #pragma unroll
-    for (int i = 0; i < 5; ++i) wg_dma16(rs, voff[i], so, b + i * 1024);
+    for (int i = 0; i < 5; ++i) wg_dma16(rs, voff[i], 0u, b + i * 1024);
   };
   f32x16 acc[2][2];
 #pragma unroll

@@ -642,13 +642,42 @@ def merge_results(first, second, num_overlap: int = 0, dim: int = 1):
     return torch.cat((first, second), dim=dim)
 
 
+def feature_aligned_encode(sd: SD, images: Tensor, enable_camera=True, enable_depth=True, enable_point=False,
+                           bf16: bool = False, agg_kwargs: Optional[dict] = None) -> dict:
+    """The context-free half of FeatureAlignedVGGT.forward: aggregator
+    (featureAligned_vggt.py:78-82), camera head (:106), depth head (:166-168),
+    point head (:183-185) -- raw outputs before any Sim(3) scaling."""
+    toks, psi = aggregator(sd, images, bf16=bf16, **(agg_kwargs or {}))
+    enc = {"tokens": toks, "patch_start_idx": psi}
+    if enable_camera:
+        enc["cam_pose_enc"] = camera_head(sd, toks)[-1]
+    if enable_depth:
+        enc["depth"], enc["depth_conf"] = dpt_head(sd, "depth_head.", toks, images, psi, "exp")
+    if enable_point:
+        enc["points"], enc["points_conf"] = dpt_head(sd, "point_head.", toks, images, psi, "inv_log")
+    return enc
+
+
 def feature_aligned_forward(sd: SD, images: Tensor, num_overlap: int, context: Optional[dict] = None,
                             gt_poses: Optional[Tensor] = None, enable_camera=True, enable_depth=True,
                             enable_point=False, num_memory_tokens: int = 8, bf16: bool = False,
                             training: bool = False, agg_kwargs: Optional[dict] = None) -> dict:
+    """FeatureAlignedVGGT.forward, featureAligned_vggt.py:48-225."""
+    enc = feature_aligned_encode(sd, images, enable_camera, enable_depth, enable_point, bf16, agg_kwargs)
+    return feature_aligned_compose(sd, enc, images, num_overlap, context, gt_poses,
+                                   num_memory_tokens=num_memory_tokens, bf16=bf16, training=training)
+
+
+def feature_aligned_compose(sd: SD, enc: dict, images: Tensor, num_overlap: int, context: Optional[dict] = None,
+                            gt_poses: Optional[Tensor] = None, num_memory_tokens: int = 8, bf16: bool = False,
+                            training: bool = False) -> dict:
+    """featureAligned_vggt.py:84-225 on given encoder outputs ``enc``
+    (feature_aligned_encode): alignment head, Sim(3)/SE(3) composition,
+    Markley mean over the overlap, scale / point transforms, context lists."""
     B, S, _, H, W = images.shape
     pred = {}
-    toks, psi = aggregator(sd, images, bf16=bf16, **(agg_kwargs or {}))
+    toks = enc["tokens"]
+    enable_camera = "cam_pose_enc" in enc
     ctx_ov = ctx_mem = None
     if context is not None:
         ctx_ov = context["overlap_tokens"]
@@ -663,7 +692,7 @@ def feature_aligned_forward(sd: SD, images: Tensor, num_overlap: int, context: O
     pf = torch.matmul(pf, chunk_se3)
     pf = torch.cat([chunk_se3, pf], dim=1)
     if enable_camera:
-        penc = camera_head(sd, toks)[-1]
+        penc = enc["cam_pose_enc"]
         extr, intr = pose_encoding_to_extri_intri(penc, (H, W))
         extr = F.pad(extr, (0, 0, 0, 1, 0, 0, 0, 0))
         extr[:, :, 3, 3] = 1.0
@@ -702,8 +731,8 @@ def feature_aligned_forward(sd: SD, images: Tensor, num_overlap: int, context: O
             if num_memory_tokens > 0:
                 context.setdefault("memory_tokens", []).append(mem)
                 pred["memory_tokens"] = context["memory_tokens"]
-    if enable_depth:
-        depth, conf = dpt_head(sd, "depth_head.", toks, images, psi, "exp")
+    if "depth" in enc:
+        depth, conf = enc["depth"], enc["depth_conf"]
         depth = depth * chunk_scale.view(B, 1, 1, 1, 1)
         if context is None:
             pred["depth"], pred["depth_conf"] = [depth], [conf]
@@ -712,8 +741,8 @@ def feature_aligned_forward(sd: SD, images: Tensor, num_overlap: int, context: O
             pred["depth"] = context["depth"]
             context.setdefault("depth_conf", []).append(conf)
             pred["depth_conf"] = context["depth_conf"]
-    if enable_point:
-        pts, pconf = dpt_head(sd, "point_head.", toks, images, psi, "inv_log")
+    if "points" in enc:
+        pts, pconf = enc["points"], enc["points_conf"]
         if enable_camera:
             if context is not None:
                 tr = closed_form_inverse_se3(pf[:, 0]).unsqueeze(1) @ pt_ident.view(B, 1, 4, 4)

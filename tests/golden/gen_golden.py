@@ -28,6 +28,7 @@ import torch
 import torch.nn.functional as F
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
 
 
 def extract(ref: str, relpath: str, names):
@@ -332,6 +333,159 @@ def gen_dinov2():
     save("dinov2_hf", **outs, **{"sd." + k: v for k, v in sd.items()})
 
 
+# ----------------------------------------------------------------------------
+# the reference-authored alignment path, run on the test-only vggt shim
+# (weights / inputs from oracle.fixture_weights, not stored)
+# ----------------------------------------------------------------------------
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+from oracle.fixture_weights import ALIGN_CASES, FA_RUNS, FIX_HW, FIX_SEED  # noqa: E402
+from oracle.fixture_weights import fa_feed, fa_gt_poses  # noqa: E402
+
+
+def _ref_alignment_modules(ref):
+    for p in (ROOT, ref):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import vggt_shim
+    vggt_shim.install()
+    from aligned_vggt.heads.alignment_head import AlignmentHead  # reference module
+    from aligned_vggt.layers.cross_attention import CrossAttentionBlock  # reference module
+    from aligned_vggt.layers.rope import RotaryPositionEmbedding  # reference module
+    from aligned_vggt.models.featureAligned_vggt import FeatureAlignedVGGT  # reference module
+    return vggt_shim, AlignmentHead, CrossAttentionBlock, RotaryPositionEmbedding, FeatureAlignedVGGT
+
+
+def gen_ref_cross_attention(ref):
+    """CrossAttentionBlock (cross_attention.py:80-131) in its two roles: a
+    decoder block (512 wide, 1 query vs S frames + 8 memory tokens) and a
+    temporal block (1024 wide, B*P groups of S queries vs T overlap keys)."""
+    shim, _, CAB, Rope, _ = _ref_alignment_modules(ref)
+    from oracle.fixture_weights import fixture_tensor, load_fixture_weights_
+    out = {}
+    S, T = 3, 2
+    seq = torch.arange(S)
+    cases = {
+        "dec": (512, (2, 1, 512), (2, 11, 512), torch.zeros(1, dtype=torch.long),
+                torch.cat([torch.arange(3), torch.arange(8) + 6])),
+        "tmp": (1024, (36, S, 1024), (36, T, 1024), seq + (S - (T - 1)), torch.cat([seq[:1], seq[-(T - 1):]])),
+    }
+    for tag, (dim, xs, ys, pq, pk) in cases.items():
+        torch.manual_seed(0)
+        blk = CAB(dim=dim, num_heads=8, mlp_ratio=4.0, qkv_bias=True, proj_bias=True, ffn_bias=True, init_values=0.01,
+                  qk_norm=True, rope=Rope(frequency=100)).eval()
+        load_fixture_weights_(blk, FIX_SEED, prefix=f"cab_{tag}.")
+        x = fixture_tensor(f"cab_{tag}.x", xs, FIX_SEED)
+        y = fixture_tensor(f"cab_{tag}.y", ys, FIX_SEED)
+        pos = (pq.view(1, -1).expand(xs[0], -1), pk.view(1, -1).expand(xs[0], -1))
+        for prec in ("f32", "bf16"):
+            with torch.no_grad(), shim.bf16_mixed(prec == "bf16"):
+                o = blk(x, y, pos=pos)
+            out[f"{tag}_{prec}"] = o.float()
+        out[f"{tag}_pos_q"], out[f"{tag}_pos_k"] = pq, pk
+    save("ref_cross_attention", **out)
+
+
+def gen_ref_alignment_head(ref):
+    """AlignmentHead.forward (alignment_head.py:224-345, eval) for first and
+    continuation chunks (T = ov + 1 overlap tokens), with and without memory,
+    B in {1, 2}, a shorter tail chunk; fp32 and emulated bf16-mixed.  Plus
+    _decode_alignments (:427-540) alone and the reference tree's parameter
+    names / shapes."""
+    import json
+    shim, AH, _, _, _ = _ref_alignment_modules(ref)
+    from oracle.fixture_weights import fixture_tensor, load_fixture_weights_
+    H, W = FIX_HW
+    P = 5 + (H // 14) * (W // 14)
+    heads = {}
+    for tag, nm in (("m8", 8), ("m0", 0)):
+        torch.manual_seed(0)
+        heads[tag] = load_fixture_weights_(AH(in_dim=2048, patch_size=14, num_memory_tokens=nm,
+                                              temporal_attention=True).eval(), FIX_SEED, prefix="alignment_head.")
+    out = {}
+    for prec in ("f32", "bf16"):
+        for case, head, B, S, nov, prev in ALIGN_CASES:
+            tok = fixture_tensor(f"ah.{case}.tokens", (B, S, P, 2048), FIX_SEED)
+            ov = out[f"{prev}_{prec}_new_ov"] if prev else None
+            mem = out.get(f"{prev}_{prec}_memory") if prev else None
+            with torch.no_grad(), shim.bf16_mixed(prec == "bf16"):
+                cs, fs, m, nov_t = heads[head](tok, (H, W), nov, overlap_tokens=ov, memory_tokens=mem)
+            out[f"{case}_{prec}_chunk_sim3"] = cs.float()
+            out[f"{case}_{prec}_frame_se3"] = fs.float()
+            if m is not None:
+                out[f"{case}_{prec}_memory"] = m.float()
+            out[f"{case}_{prec}_new_ov"] = nov_t.float()
+    # _decode_alignments alone (fp32: autocast is off there in the reference)
+    h = heads["m8"]
+    ft = fixture_tensor("dec.tokens1", (2, 4, 1024), FIX_SEED)
+    with torch.no_grad():
+        d1 = h._decode_alignments(ft, 2, True, memory_tokens=None)
+        ft2 = fixture_tensor("dec.tokens2", (2, 4, 1024), FIX_SEED)
+        d2 = h._decode_alignments(ft2, 2, False, memory_tokens=d1[2])
+    for i, d in ((1, d1), (2, d2)):
+        for name, v in zip(("chunk_sim3", "frame_se3", "memory"), d):
+            out[f"dec{i}_{name}"] = v.float()
+    save("ref_alignment_head", **out)
+    keys = {tag: [[k, list(v.shape)] for k, v in hd.state_dict().items()] for tag, hd in heads.items()}
+    with open(os.path.join(HERE, "ref_alignment_keys.json"), "w") as f:
+        json.dump(keys, f)
+    print("wrote ref_alignment_keys.json", {k: len(v) for k, v in keys.items()})
+
+
+def gen_ref_feature_aligned(ref):
+    """FeatureAlignedVGGT.forward composition (featureAligned_vggt.py:73-225) over
+    whole chunk sequences: the reference's alignment head + Sim(3)/SE(3)
+    composition + Markley mean + context bookkeeping, with stub encoders
+    returning fixed outputs.  Dense maps are stored at every 7th pixel."""
+    import json
+    shim, _, _, _, FA = _ref_alignment_modules(ref)
+    from oracle import vggt_oracle as O
+    from oracle.fixture_weights import fixture_tensor, load_fixture_weights_
+    H, W = FIX_HW
+    torch.manual_seed(0)
+    fa = FA(img_size=518, patch_size=14, embed_dim=1024, enable_camera=True, enable_point=True, enable_depth=True,
+            enable_track=False, num_memory_tokens=8).eval()
+    load_fixture_weights_(fa.alignment_head, FIX_SEED, prefix="alignment_head.")
+    out = {}
+    for prec in ("f32", "bf16"):
+        for run, N, w, ov, use_gt in FA_RUNS:
+            imgs = fixture_tensor(f"fa.{run}.images", (1, N, 3, H, W), FIX_SEED, "uniform")
+            ctx = None
+            chunks = O.generate_chunks(N, w, ov)
+            for i, ids in enumerate(chunks):
+                feed = fa_feed(run, i, len(ids))
+                shim._Feed.tokens = feed["tokens"]
+                for k in ("pose_enc", "depth", "depth_conf", "points", "points_conf"):
+                    setattr(shim._Feed, k, feed[k])
+                gt = fa_gt_poses(run, i, len(ids)) if use_gt else None
+                with torch.no_grad(), shim.bf16_mixed(prec == "bf16"):
+                    ctx = fa(imgs[:, ids], ov, ctx, gt_poses=gt)
+            p = f"{run}_{prec}_"
+            for i in range(len(chunks)):
+                out[p + f"pose_enc{i}"] = ctx["pose_enc"][i]
+                out[p + f"memory{i}"] = ctx["memory_tokens"][i]
+                out[p + f"depth{i}"] = ctx["depth"][i][:, :, ::7, ::7]
+                out[p + f"depth_conf{i}"] = ctx["depth_conf"][i][:, :, ::7, ::7]
+                out[p + f"points{i}"] = ctx["world_points"][i][:, :, ::7, ::7]
+                out[p + f"points_conf{i}"] = ctx["world_points_conf"][i][:, :, ::7, ::7]
+            out[p + "chunk_sim3"] = ctx["chunk_sim3_alignment_enc"]
+            out[p + "frame_se3"] = ctx["frame_se3_alignment_enc"]
+            out[p + "overlap_tokens"] = ctx["overlap_tokens"]
+            out[p + "nchunks"] = np.array(len(chunks))
+    save("ref_feature_aligned", **out)
+    # set_config (featureAligned_vggt.py:34-46) rebuilds the alignment head
+    from types import SimpleNamespace
+    cfg = SimpleNamespace(enable_camera=True, enable_point=False, enable_depth=True, enable_track=False,
+                          num_memory_tokens=0, patch_size=14, temporal_attention=True)
+    fa.set_config(cfg)
+    info = {"cfg": vars(cfg), "keys": [[k, list(v.shape)] for k, v in fa.state_dict().items()],
+            "heads_none": [n for n in ("camera_head", "point_head", "depth_head", "track_head")
+                           if getattr(fa, n) is None], "enable_memory": fa.enable_memory}
+    with open(os.path.join(HERE, "ref_set_config.json"), "w") as f:
+        json.dump(info, f)
+    print("wrote ref_set_config.json", len(info["keys"]), info["heads_none"])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -352,6 +506,9 @@ def main():
     gen_scale_alignment(a.ref)
     gen_small_fns(a.ref)
     gen_dinov2()
+    gen_ref_cross_attention(a.ref)
+    gen_ref_alignment_head(a.ref)
+    gen_ref_feature_aligned(a.ref)
 
 
 if __name__ == "__main__":

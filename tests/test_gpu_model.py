@@ -129,6 +129,30 @@ def test_dpt_presplit_bitwise(models):
     assert torch.equal(outs["bf16x3"][1], outs["bf16x3pre"][1])
 
 
+def test_dpt_frame_groups_match(models, monkeypatch):
+    """A chunk whose widest DPT map would pass the convolutions' 32-bit offsets
+    runs in groups of frames: with the bound lowered so 3 frames
+    split 2 + 1 (and B = 2 chunks split across the batch boundary), the outputs
+    equal the one-launch form."""
+    m, sd = models
+    from aligned_vggt.backbone import dpt_head as D
+    from aligned_vggt.utils.synthetic import synthetic_images
+    imgs = synthetic_images(2, 3, 56, 70, seed=14)
+    toks, psi = O.aggregator(sd, imgs, bf16=True)
+    tg = [t.cuda() for t in toks]
+    scale = torch.tensor([1.5, 0.75], device="cuda")
+    full = m.depth_head(tg, images=imgs.cuda(), patch_start_idx=psi, _scale=scale)
+    monkeypatch.setattr(D, "MAP_BYTES_LIMIT", 2 * 56 * 70 * 128 * 2 + 1)
+    grouped = m.depth_head(tg, images=imgs.cuda(), patch_start_idx=psi, _scale=scale)
+    for a, b in zip(grouped, full):
+        assert a.shape == b.shape
+        assert _rel(a, b) < 1e-6
+    # and a single chunk (B = 1) past the bound
+    one = m.depth_head([t[:1] for t in tg], images=imgs[:1].cuda(), patch_start_idx=psi, _scale=scale[:1])
+    for a, b in zip(one, full):
+        assert _rel(a, b[:1]) < 1e-6
+
+
 def test_alignment_head_bf16_tier(models):
     m, sd = models
     from aligned_vggt.utils.synthetic import synthetic_images

@@ -267,6 +267,26 @@ def test_bf16_weight_grad(N, M, Nn, K):
     assert _rel(out3, ref) < 4e-3
 
 
+@pytest.mark.parametrize("M,Nn,K", [(6870, 1024, 1024), (77, 1024, 1024), (1000, 3072, 1024), (22001, 1024, 4096)])
+def test_bf16_weight_grad_nan_guard(N, M, Nn, K):
+    """dY / X are row slices of larger NaN-filled buffers with M % 32 != 0 and
+    several token splits: the ragged last tile of each split and the surplus
+    prefetch tiles must read zeros, never the NaN rows behind the slice
+    (the DMA descriptor range check ignores soffset)."""
+    torch.manual_seed(9)
+    pad = 96
+    dyb = torch.full((M + 2 * pad, Nn), float("nan"), device="cuda", dtype=torch.bfloat16)
+    xb = torch.full((M + 2 * pad, K), float("nan"), device="cuda", dtype=torch.bfloat16)
+    dy, x = dyb[pad:pad + M], xb[pad:pad + M]
+    dy.copy_(torch.randn(M, Nn, device="cuda"))
+    x.copy_(torch.randn(M, K, device="cuda"))
+    ref = dy.float().t() @ x.float()
+    out = torch.empty(Nn, K, device="cuda")
+    N.wgrad_bf16(dy, x, out, False)
+    assert bool(torch.isfinite(out).all())
+    assert _rel(out, ref) < 4e-3
+
+
 # ------------------------------------------------------------------ blocks / head vs oracle autograd
 def _head_and_sd(seed=11, nm=8):
     from aligned_vggt.heads.alignment_head import AlignmentHead
