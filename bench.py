@@ -4,12 +4,16 @@ ViT-L/14-reg + 24 frame + 24 global alternating-attention blocks) forward on
 one 16-frame 518x518 synthetic chunk (BASELINE.json configs[1]), bf16 MFMA,
 random-init weights.
 
-  python bench.py [--gpus N --steps K --warmup W] [--workload aggregator|chunk]
+  python bench.py [--gpus N --steps K --warmup W] [--workload aggregator|chunk|sequence|train]
+  python bench.py --config 3 --gpus 8     (BASELINE configs[3]: 512 frames 154x518, chunk 16 / overlap 4)
 
-N > 1: one process per GPU (torch.distributed over RCCL, launched by
-torch.distributed.run); every rank runs its own independent chunks (the
-encoder does not shard -- replicas, weak scaling), value = all ranks' chunks
-/ max-over-ranks time.  Prints ONE JSON line on rank 0 with the roofline of
+N > 1: one process per GPU (torch.distributed over RCCL).  Run as is, bench.py
+starts ``python -m torch.distributed.run --nproc-per-node N`` itself (before
+touching the GPU) and relays rank 0's line; under an external torchrun it
+reads RANK / WORLD_SIZE.  aggregator / chunk / train: every rank runs its own
+independent chunks (replicas, weak scaling), value = all ranks' chunks /
+max-over-ranks time; sequence: the ranks share one sequence through the
+ChunkPipeline baton ring (strong scaling).  Prints ONE JSON line on rank 0 with the roofline of
 the dominant kernel (global attention) measured with HIP events on the
 stream it is launched on, and the CPU baseline (the oracle's fp32 path on a
 bounded sample of the same workload).
@@ -19,6 +23,9 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -50,12 +57,15 @@ def agg_flops(S=S_FRAMES, H=H_IMG, W=W_IMG, C=1024, depth=24, dino_depth=24):
 
 def cpu_baseline(threads: int):
     """Time the oracle (reference numerics, fp32, CPU) on a bounded sample of
-    the SAME workload: one DINOv2 block, one frame block and one global block
-    at the full 16x518x518 chunk shape; scale to a whole chunk by the layer
-    counts (24 each; patch-embed/LN glue < 0.1% of FLOPs is not counted)."""
+    the SAME workload at the full 16x518x518 chunk shape: the DINOv2 patch
+    embed + final LayerNorm, one DINOv2 block, one frame block, one global
+    block and the four kept-layer concats; the whole chunk = patch embed +
+    24 x each block kind + concats.  Threads: the GPU box's per-GPU CPU share
+    (16), not the whole host (os.cpu_count() reports every CPU of the
+    machine, shared with other jobs)."""
     from oracle import vggt_oracle as O
     from aligned_vggt.backbone.aggregator import Aggregator
-    from aligned_vggt.utils.synthetic import synthetic_init_
+    from aligned_vggt.utils.synthetic import synthetic_images, synthetic_init_
     torch.set_num_threads(threads)
     agg = Aggregator(depth=1, dino_depth=1)
     synthetic_init_(agg)
@@ -64,20 +74,64 @@ def cpu_baseline(threads: int):
     P = 5 + hw
     g = torch.Generator().manual_seed(0)
     x = torch.randn(S_FRAMES, P, 1024, generator=g)
+    imgs = synthetic_images(1, S_FRAMES, H_IMG, W_IMG)[0]
     pos = O.position_grid(S_FRAMES, H_IMG // 14, W_IMG // 14, 5)
     with torch.no_grad():
         t0 = time.perf_counter()
-        O.block(sd, "aggregator.patch_embed.blocks.0.", x, 16, eps=1e-6)
+        O.dinov2(sd, "aggregator.patch_embed.", imgs, False, depth=0)
         t1 = time.perf_counter()
-        O.block(sd, "aggregator.frame_blocks.0.", x, 16, pos, "2d", True)
+        O.block(sd, "aggregator.patch_embed.blocks.0.", x, 16, eps=1e-6)
         t2 = time.perf_counter()
-        O.block(sd, "aggregator.global_blocks.0.", x.view(1, S_FRAMES * P, 1024), 16, pos.view(1, -1, 2), "2d", True)
+        O.block(sd, "aggregator.frame_blocks.0.", x, 16, pos, "2d", True)
         t3 = time.perf_counter()
-    sec_chunk = 24 * (t1 - t0) + 24 * (t2 - t1) + 24 * (t3 - t2)
+        O.block(sd, "aggregator.global_blocks.0.", x.view(1, S_FRAMES * P, 1024), 16, pos.view(1, -1, 2), "2d", True)
+        t4 = time.perf_counter()
+        for _ in range(4):
+            torch.cat([x, x], dim=-1)
+        t5 = time.perf_counter()
+    sec_chunk = (t1 - t0) + 24 * (t2 - t1) + 24 * (t3 - t2) + 24 * (t4 - t3) + (t5 - t4)
     return {"value": 1.0 / sec_chunk, "unit": "chunks/s", "cores": threads, "kind": "port",
-            "sample": f"oracle fp32 CPU (reference numerics): 1 DINOv2 + 1 frame + 1 global block at 16x518x518 "
-                      f"({t3 - t0:.1f} s measured), scaled x24 each to a full aggregator chunk "
-                      f"({sec_chunk:.1f} s/chunk)"}
+            "host_cpu": _cpu_model(), "host_logical_cpus": os.cpu_count(),
+            "sample": f"oracle fp32 CPU (reference numerics) at 16x518x518: patch embed + final LN, 1 DINOv2 + "
+                      f"1 frame + 1 global block, 4 kept-layer concats ({t5 - t0:.1f} s measured); blocks scaled "
+                      f"x24 each to a full aggregator chunk ({sec_chunk:.1f} s/chunk)"}
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _launch(args) -> int:
+    """--gpus N > 1 without a torchrun environment: start N ranks with
+    torch.distributed.run as a CHILD process (the parent never touches the
+    GPU, so no exec after HIP init) and return its exit code; rank 0's JSON
+    line reaches stdout through it."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+# BASELINE.json configs as presets: (workload, seq_frames, height, frames, overlap, memory tokens)
+CONFIGS = {1: ("aggregator", None, 518, 16, 4, 8), 2: ("sequence", 64, 518, 16, 4, 8),
+           3: ("sequence", 512, 154, 16, 4, 0), 4: ("sequence", 512, 154, 16, 4, 8)}
 
 
 class EventTimer:
@@ -112,12 +166,17 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="aggregator", choices=["aggregator", "chunk", "sequence", "train"],
+    ap.add_argument("--config", type=int, default=None, choices=sorted(CONFIGS),
+                    help="BASELINE.json configs[i] preset (sets workload / frames / size / memory)")
+    ap.add_argument("--memory-tokens", type=int, default=8, help="alignment-head memory tokens (0: no memory)")
+    ap.add_argument("--workload", default="aggregator",
+                    choices=["aggregator", "chunk", "sequence", "train", "selftest"],
                     help="aggregator: BASELINE configs[1] headline (default); chunk: full FeatureAlignedVGGT "
                          "per-chunk forward (encoder + alignment head + camera/depth heads); sequence: configs[2..4] "
                          "chunk pipeline over --seq-frames frames (RCCL baton ring at N>1); train: one alignment-head "
                          "training step (two chunks with memory recurrence, forward + backward + AdamW) on resident "
-                         "synthetic aggregator tokens (SURVEY §8f row 4)")
+                         "synthetic aggregator tokens (SURVEY §8f row 4); selftest: the multi-rank launcher and "
+                         "baton ring on CPU / gloo with a toy model (no GPU)")
     ap.add_argument("--seq-frames", type=int, default=64)
     ap.add_argument("--height", type=int, default=H_IMG)
     ap.add_argument("--overlap", type=int, default=4)
@@ -125,10 +184,21 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
     args = ap.parse_args()
+    if args.config is not None:
+        args.workload, seq, args.height, args.frames, args.overlap, args.memory_tokens = CONFIGS[args.config]
+        if seq is not None:
+            args.seq_frames = seq
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; using the launcher's {world} ranks",
+              file=sys.stderr)
+    if args.workload == "selftest":
+        return bench_selftest(args, world, rank)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -241,7 +311,8 @@ def bench_full(args, world, rank, dev):
     from aligned_vggt.models.featureAligned_vggt import FeatureAlignedVGGT
     from aligned_vggt.utils.data import generate_chunks
     from aligned_vggt.utils.synthetic import condition_pose_outputs_, synthetic_images, synthetic_init_
-    model = FeatureAlignedVGGT(enable_point=False, enable_track=False, num_memory_tokens=8).to(dev).eval()
+    nm = args.memory_tokens
+    model = FeatureAlignedVGGT(enable_point=False, enable_track=False, num_memory_tokens=nm).to(dev).eval()
     synthetic_init_(model, seed=0)
     condition_pose_outputs_(model)
     H, W = args.height, W_IMG
@@ -264,7 +335,7 @@ def bench_full(args, world, rank, dev):
         P1 = 6 + (H // 14) * (W // 14)
 
         def step():
-            pipe.run(seq, S, ov, token_dims=(P1, 1024), memory_shape=(1, 8, 512))
+            pipe.run(seq, S, ov, token_dims=(P1, 1024), memory_shape=(1, nm, 512) if nm > 0 else None)
         n_chunks_step = len(generate_chunks(args.seq_frames, "chunk_overlap", S, ov))
     for _ in range(args.warmup):
         step()
@@ -290,9 +361,13 @@ def bench_full(args, world, rank, dev):
             "value": round(value, 4), "unit": "chunks/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak" if args.workload == "chunk" else "strong", "vs_baseline": None, "dtype": "bf16",
-            "data": "synthetic", "config": {"workload": args.workload, "frames": S, "overlap": ov,
+            "data": "synthetic", "config": {"workload": args.workload, "baseline_config": args.config,
+                                            "frames": S, "overlap": ov,
                                             "seq_frames": args.seq_frames if args.workload == "sequence" else None,
-                                            "image": [H, W], "heads": "camera+depth+alignment(memory 8)"}}),
+                                            "image": [H, W], "heads": "camera+depth+alignment(memory %d)" % nm,
+                                            "parallelism": ("chunk pipeline x%d (RCCL baton ring)" % world
+                                                            if args.workload == "sequence" else
+                                                            "replicas x%d" % world)}}),
               flush=True)
 
 
@@ -366,6 +441,48 @@ def bench_train(args, world, rank, dev):
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (resident encoder tokens)",
             "config": {"workload": "train", "frames": S, "overlap": ov, "image": [H, W],
                        "chunks_per_step": 2, "parallelism": "dp%d" % world}}), flush=True)
+
+
+def bench_selftest(args, world, rank):
+    """CPU / gloo check of the multi-rank path end to end (launcher ->
+    torch.distributed.run -> N ranks -> ChunkPipeline baton ring ->
+    max-over-ranks timing -> one JSON line from rank 0) with the toy model of
+    tests/toy_model.py; no GPU is touched."""
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from toy_model import C, DEC, NMEM, P1, ToyAlignModel
+    from aligned_vggt.dist.pipeline import ChunkPipeline
+    from aligned_vggt.utils.data import generate_chunks
+    if world > 1:
+        dist.init_process_group("gloo")
+    g = torch.Generator().manual_seed(0)
+    seq = torch.rand(2, args.seq_frames, 3, 4, 5, generator=g)
+    pipe = ChunkPipeline(ToyAlignModel(), device=torch.device("cpu"), gather_dense=True)
+    run = lambda: pipe.run(seq, args.frames, args.overlap, token_dims=(P1, C), memory_shape=(2, NMEM, DEC))  # noqa
+    for _ in range(args.warmup):
+        run()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = run()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt])
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+        dist.destroy_process_group()
+    if rank == 0:
+        n = len(generate_chunks(args.seq_frames, "chunk_overlap", args.frames, args.overlap))
+        print(json.dumps({"metric": "selftest chunks/sec (toy model, CPU gloo)", "value": round(n * args.steps / dt, 4),
+                          "unit": "chunks/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+                          "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                          "config": {"workload": "selftest", "seq_frames": args.seq_frames, "frames": args.frames,
+                                     "overlap": args.overlap},
+                          "checksum": {k: round(float(v.double().sum()), 6) for k, v in out.items()}}), flush=True)
 
 
 if __name__ == "__main__":

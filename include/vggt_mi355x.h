@@ -354,6 +354,29 @@ int vggt_sim3_points(const float* pts, int64_t p_bs, int B, int64_t n, const flo
  * featureAligned_vggt.py:171; pointAligned_wrapped_vggt.py:130-132). */
 int vggt_scale_f32(float* x, int64_t bs, int B, int64_t n, const float* scale, void* stream);
 
+/*
+ * Per-chunk pose / Sim(3) composition of FeatureAlignedVGGT.forward
+ * (featureAligned_vggt.py:96-143 and the point transform of :187-196), one
+ * launch, no host synchronisation:
+ *   chunk_se3 = pose_encoding_to_extri(chunk_sim3[:7]), scale = chunk_sim3[7];
+ *   per_frame_se3 = [chunk_se3, pose_encoding_to_extri(frame_se3[f]) @ chunk_se3];
+ *   extr = camera extrinsics (pose_encoding_to_extri_intri of cam_pose_enc)
+ *          @ inv(extr[0]), translation * scale;
+ *   mean = I (no context) | gt_first[b] | Markley mean over the overlap of
+ *          inv(extr[k]) @ pose_encoding_to_extri(ctx_pose_enc[S_prev-ov+k])
+ *          (averagePoseEncodings, geometry.py:4-37; ov == 1: the one transform);
+ *   aligned_pose_enc = extri_intri_to_pose_encoding(extr @ (per_frame_se3 @ mean)).
+ * chunk_sim3 [B,8], frame_se3 [B,S-1,7], cam_pose_enc [B,S,9] (T, quat xyzw,
+ * FoV h/w), ctx_pose_enc [B,S_prev,9] = context["pose_enc"][-1] or NULL (first
+ * chunk), gt_first [B,4,4] = gt_poses[:, 0] or NULL; all fp32 contiguous device.
+ * Outputs aligned_pose_enc [B,S,9]; point_transform [B,4,4] (or NULL) =
+ * context ? inv(per_frame_se3[:,0]) @ extr_raw[:,0] : extr_raw[:,0].
+ * Requires 1 <= overlap <= min(S, S_prev, 64) when the Markley path runs.
+ */
+int vggt_pose_compose(const float* chunk_sim3, const float* frame_se3, const float* cam_pose_enc,
+                      const float* ctx_pose_enc, int S_prev, const float* gt_first, int B, int S, int overlap, int H,
+                      int W, float* aligned_pose_enc, float* point_transform, void* stream);
+
 /* ======================================================================
  * Training (backward) entry points -- alignment-head training, SURVEY.md §8f
  * row 4: train_featureAlignedVGGT_vkitti.yaml freezes the aggregator, camera

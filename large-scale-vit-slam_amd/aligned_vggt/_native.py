@@ -62,6 +62,7 @@ _SIGS = {
                        ctypes.c_size_t, _vp],
     "vggt_sim3_points": [_vp, _i64, _i, _i64, _vp, _vp, _vp, _i64, _vp],
     "vggt_scale_f32": [_vp, _i64, _i, _i64, _vp, _vp],
+    "vggt_pose_compose": [_vp, _vp, _vp, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp],
     # training (backward) entry points
     "vggt_attention_fwd_lse": [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i, _i, _i,
                                _i, _i, _f, _vp],
@@ -541,6 +542,27 @@ def sim3_points(pts: torch.Tensor, T: torch.Tensor, scale: Optional[torch.Tensor
                                 _stream())
     _check(rc, "vggt_sim3_points")
     return out
+
+
+def pose_compose(chunk_sim3: torch.Tensor, frame_se3: torch.Tensor, cam_pose_enc: torch.Tensor,
+                 ctx_pose_enc: Optional[torch.Tensor], gt_first: Optional[torch.Tensor], overlap: int,
+                 image_hw, want_point_transform: bool = True):
+    """featureAligned_vggt.py:96-143 (+ the point transform of :187-196) in one
+    launch -> (aligned_pose_enc (B,S,9), point_transform (B,4,4) or None)."""
+    _dev(cam_pose_enc, "pose_compose")
+    dev = cam_pose_enc.device
+    B, S = cam_pose_enc.shape[:2]
+    f32 = lambda t: t.to(device=dev, dtype=torch.float32).contiguous() if t is not None else None  # noqa: E731
+    cs, fs, cam = f32(chunk_sim3.reshape(B, 8)), f32(frame_se3.reshape(B, S - 1, 7)), f32(cam_pose_enc)
+    ctx = f32(ctx_pose_enc)
+    gt = f32(gt_first.reshape(B, 4, 4)) if gt_first is not None else None
+    out = torch.empty(B, S, 9, device=dev)
+    pt = torch.empty(B, 4, 4, device=dev) if want_point_transform else None
+    H, W = int(image_hw[0]), int(image_hw[1])
+    rc = lib().vggt_pose_compose(_p(cs), _p(fs), _p(cam), _p(ctx), ctx.shape[1] if ctx is not None else 0, _p(gt),
+                                 B, S, int(overlap), H, W, _p(out), _p(pt), _stream())
+    _check(rc, "vggt_pose_compose")
+    return out, pt
 
 
 def scale_(x: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:

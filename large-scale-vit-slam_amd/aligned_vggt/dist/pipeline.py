@@ -28,6 +28,7 @@ points) stay on the rank that produced them unless ``gather_dense``.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from typing import Dict, List, Optional
 
@@ -130,6 +131,20 @@ def _split_batch(enc: dict, B: int, n: int) -> List[dict]:
     return outs
 
 
+def _record_stream(obj, stream) -> None:
+    """Mark every device tensor in obj (dict / list nesting) as used on
+    ``stream`` so the caching allocator keeps it until that stream is done."""
+    if torch.is_tensor(obj):
+        if obj.is_cuda:
+            obj.record_stream(stream)
+    elif isinstance(obj, dict):
+        for v in obj.values():
+            _record_stream(v, stream)
+    elif isinstance(obj, (list, tuple)):
+        for v in obj:
+            _record_stream(v, stream)
+
+
 def _overlap_of(S: int, num_overlap: int) -> int:
     """featureAligned_vggt.py:93."""
     return num_overlap if S > num_overlap else S - 1
@@ -156,11 +171,11 @@ class ChunkPipeline:
         # on 256 CUs) fill the GPU poorly one at a time: configs[3] 1637 ->
         # 1415-1466 ms per 43 chunks in groups of 3; 518^2 chunks in pairs: the
         # GEMM / attention rounds quantise better (profiles/r4/encode_groups.md).
-        # Single rank only: on W > 1 ranks an early encode would delay the baton.
-        # VGGT_ENCODE_GROUP sets the default.
+        # On W > 1 ranks a group is a run of the rank's OWN consecutive chunks
+        # (i, i + W, ...).  VGGT_ENCODE_GROUP sets the default.
         if encode_group is None:
             encode_group = int(os.environ.get("VGGT_ENCODE_GROUP", "3"))
-        self.encode_group = max(1, encode_group) if self.world == 1 else 1
+        self.encode_group = max(1, encode_group)
 
     # ----------------------------------------------------- frame transfer
     def _fetch(self, images: torch.Tensor, idx):
@@ -204,18 +219,34 @@ class ChunkPipeline:
             shapes["memory_tokens"] = mem
         return shapes
 
-    def _send(self, ctx: dict, dst: int, keys):
-        for k in keys:
-            t = ctx[k][-1] if isinstance(ctx[k], list) else ctx[k]
-            dist.send(t.contiguous().to(self.device), dst, group=self.group)
+    def _isend(self, ctx: dict, dst: int, keys):
+        """Post the baton's tensors to ``dst`` (RCCL: on its own stream, after
+        the current stream's queued work); returns (works, tensors) -- the
+        tensors must stay alive until the works complete."""
+        ts = [(ctx[k][-1] if isinstance(ctx[k], list) else ctx[k]).contiguous().to(self.device) for k in keys]
+        ops = [dist.P2POp(dist.isend, t, dst, group=self.group) for t in ts]
+        return dist.batch_isend_irecv(ops), ts
 
-    def _recv(self, src: int, shapes: Dict[str, tuple]) -> dict:
-        out = {}
-        for k, shp in shapes.items():
-            t = torch.empty(shp, device=self.device, dtype=torch.float32)
-            dist.recv(t, src, group=self.group)
-            out[k] = t
-        return out
+    def _irecv(self, src: int, shapes: Dict[str, tuple]):
+        out = {k: torch.empty(shp, device=self.device, dtype=torch.float32) for k, shp in shapes.items()}
+        ops = [dist.P2POp(dist.irecv, t, src, group=self.group) for t in out.values()]
+        return dist.batch_isend_irecv(ops), out
+
+    def _p2p_warmup(self):
+        """Create the ring's point-to-point communicators up front (RCCL builds
+        a pair's communicator on its first send/recv, blocking both hosts until
+        the peer joins -- inside the timed loop that would stall the enqueue of
+        the next encode)."""
+        if self.world == 1 or self.__dict__.get("_p2p_ready"):
+            return
+        W, r = self.world, self.rank
+        a = torch.zeros(1, device=self.device)
+        b = torch.zeros(1, device=self.device)
+        ops = [dist.P2POp(dist.isend, a, (r + 1) % W, group=self.group),
+               dist.P2POp(dist.irecv, b, (r - 1) % W, group=self.group)]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        self._p2p_ready = True
 
     # ---------------------------------------------------------------- run
     @torch.no_grad()
@@ -229,59 +260,136 @@ class ChunkPipeline:
         None elsewhere."""
         B, Nf = images.shape[:2]
         chunks = generate_chunks(Nf, "chunk_overlap", chunk_width, num_overlap)
-        n = len(chunks)
-        W, r = self.world, self.rank
-        P1, C = token_dims
         keys = ["overlap_tokens", "pose_enc"] + (["memory_tokens"] if memory_shape is not None else [])
-        mine: Dict[int, dict] = {}
-        local = None  # baton kept in memory when the next chunk stays on this rank (W == 1)
-        my = list(range(r, n, W))
-        # encode groups (one rank: every chunk is ours, in order)
-        groups = (_encode_groups([len(c) for c in chunks], images, self.model, self.encode_group)
-                  if W == 1 else [[i] for i in my])
+        if self.world == 1:
+            mine = self._run_local(images, chunks, num_overlap, keys, memory_shape, B)
+        else:
+            mine = self._run_ring(images, chunks, num_overlap, keys, token_dims, memory_shape, B)
+        return self._gather(mine, chunks, num_overlap, B)
+
+    def _groups(self, chunks, own: List[int], images) -> List[List[int]]:
+        """Encode groups over this rank's own chunks (runs of equal length)."""
+        g = _encode_groups([len(chunks[i]) for i in own], images, self.model, self.encode_group)
+        return [[own[j] for j in grp] for grp in g]
+
+    def _encode(self, images, chunks, g: List[int], frames) -> Dict[int, dict]:
+        xs = [self._ready(f) for f in frames]
+        B = xs[0].shape[0]
+        if len(g) == 1:
+            return {g[0]: self.model.encode_chunk(xs[0])}
+        return dict(zip(g, _split_batch(self.model.encode_chunk(torch.cat(xs, 0)), B, len(g))))
+
+    @staticmethod
+    def _summary(pred: dict, S: int) -> dict:
+        out = {"pose_enc": pred["pose_enc"][-1], "chunk_sim3": pred["chunk_sim3_alignment_enc"][:, -1:],
+               "frame_se3": pred["frame_se3_alignment_enc"][:, -(S - 1):] if S > 1
+               else pred["frame_se3_alignment_enc"][:, :0]}
+        if "depth" in pred:
+            out["depth"] = pred["depth"][-1]
+            out["depth_conf"] = pred["depth_conf"][-1]
+        return out
+
+    def _ctx_from(self, ctx_in: dict, B: int, memory_shape) -> dict:
+        ctx = {"overlap_tokens": ctx_in["overlap_tokens"], "pose_enc": [ctx_in["pose_enc"]],
+               "chunk_sim3_alignment_enc": torch.zeros(B, 0, 8, device=self.device),
+               "frame_se3_alignment_enc": torch.zeros(B, 0, 7, device=self.device)}
+        if memory_shape is not None:
+            ctx["memory_tokens"] = [ctx_in["memory_tokens"]]
+        return ctx
+
+    def _run_local(self, images, chunks, num_overlap, keys, memory_shape, B) -> Dict[int, dict]:
+        """One rank: every chunk in order, the baton kept in memory; the next
+        group's frames prefetched while the current group runs."""
+        n = len(chunks)
+        groups = self._groups(chunks, list(range(n)), images)
         fetch = lambda g: [self._fetch(images, chunks[i]) for i in g]  # noqa: E731
         nxt = fetch(groups[0]) if groups else None
+        mine: Dict[int, dict] = {}
         encs: Dict[int, dict] = {}
+        local = None
         gi = 0
-        for j, i in enumerate(my):
+        for i in range(n):
             if i not in encs:
-                # this group's frames (prefetched while the previous group ran), the
-                # next group's transfer queued behind them
-                xs = [self._ready(f) for f in nxt]
-                g = groups[gi]
+                frames, g = nxt, groups[gi]
                 gi += 1
                 nxt = fetch(groups[gi]) if gi < len(groups) else None
-                if len(g) == 1:
-                    encs[i] = self.model.encode_chunk(xs[0])
-                else:
-                    encs.update(zip(g, _split_batch(self.model.encode_chunk(torch.cat(xs, 0)), B, len(g))))
-            enc = encs.pop(i)
-            ctx = None
-            if i > 0:
-                Sp = len(chunks[i - 1])
-                if W == 1:
-                    ctx_in = local
-                else:
-                    ctx_in = self._recv((i - 1) % W, self._baton_shapes(B, Sp, _overlap_of(Sp, num_overlap), P1, C,
-                                                                       memory_shape))
-                ctx = {"overlap_tokens": ctx_in["overlap_tokens"], "pose_enc": [ctx_in["pose_enc"]],
-                       "chunk_sim3_alignment_enc": torch.zeros(B, 0, 8, device=self.device),
-                       "frame_se3_alignment_enc": torch.zeros(B, 0, 7, device=self.device)}
-                if memory_shape is not None:
-                    ctx["memory_tokens"] = [ctx_in["memory_tokens"]]
-            pred = self.model.align_chunk(enc, num_overlap, ctx)
+                encs.update(self._encode(images, chunks, g, frames))
+            ctx = self._ctx_from(local, B, memory_shape) if i > 0 else None
+            pred = self.model.align_chunk(encs.pop(i), num_overlap, ctx)
             if i + 1 < n:
-                if W == 1:
-                    local = {k: (pred[k][-1] if isinstance(pred[k], list) else pred[k]) for k in keys}
-                else:
-                    self._send(pred, (i + 1) % W, keys)
-            mine[i] = {"pose_enc": pred["pose_enc"][-1], "chunk_sim3": pred["chunk_sim3_alignment_enc"][:, -1:],
-                       "frame_se3": pred["frame_se3_alignment_enc"][:, -(len(chunks[i]) - 1):]
-                       if len(chunks[i]) > 1 else pred["frame_se3_alignment_enc"][:, :0]}
-            if "depth" in pred:
-                mine[i]["depth"] = pred["depth"][-1]
-                mine[i]["depth_conf"] = pred["depth_conf"][-1]
-        return self._gather(mine, chunks, num_overlap, B)
+                local = {k: (pred[k][-1] if isinstance(pred[k], list) else pred[k]) for k in keys}
+            mine[i] = self._summary(pred, len(chunks[i]))
+        return mine
+
+    def _run_ring(self, images, chunks, num_overlap, keys, token_dims, memory_shape, B) -> Dict[int, dict]:
+        """W > 1 ranks: rank r owns chunks r, r + W, ...  Encodes run on the
+        compute stream one group ahead; each alignment runs on a side stream
+        that waits (device-side) for its encode and for the baton from rank
+        i - 1 (irecv posted early), and posts the baton to rank i + 1 (isend)
+        as soon as it is done -- the host never blocks on a peer, and the
+        compute stream keeps encoding while a baton is in flight."""
+        W, r = self.world, self.rank
+        n = len(chunks)
+        P1, C = token_dims
+        cuda = self.device is not None and torch.device(self.device).type == "cuda"
+        self._p2p_warmup()
+        own = list(range(r, n, W))
+        groups = self._groups(chunks, own, images)
+        group_of = {i: gi for gi, g in enumerate(groups) for i in g}
+        side = None
+        if cuda:
+            side = self.__dict__.get("_align_stream")
+            if side is None:
+                lo, hi = torch.cuda.Stream.priority_range()
+                side = self._align_stream = torch.cuda.Stream(self.device, priority=hi)
+        main = torch.cuda.current_stream(self.device) if cuda else None
+        encs: Dict[int, dict] = {}
+        ready: Dict[int, object] = {}
+        enqueued = 0
+
+        def enqueue(gi):
+            g = groups[gi]
+            out = self._encode(images, chunks, g, [self._fetch(images, chunks[i]) for i in g])
+            ev = None
+            if cuda:
+                ev = torch.cuda.Event()
+                ev.record(main)
+            for i in g:
+                encs[i] = out[i]
+                ready[i] = ev
+
+        mine: Dict[int, dict] = {}
+        sends = []
+        for i in own:
+            gi = group_of[i]
+            while enqueued <= min(gi + 1, len(groups) - 1):  # this group and the next one queued
+                enqueue(enqueued)
+                enqueued += 1
+            enc = encs.pop(i)
+            with (torch.cuda.stream(side) if cuda else contextlib.nullcontext()):
+                if cuda:
+                    side.wait_event(ready.pop(i))
+                    _record_stream(enc, side)
+                ctx = None
+                if i > 0:
+                    Sp = len(chunks[i - 1])
+                    works, ctx_in = self._irecv((i - 1) % W, self._baton_shapes(
+                        B, Sp, _overlap_of(Sp, num_overlap), P1, C, memory_shape))
+                    for w in works:
+                        w.wait()  # RCCL: the side stream waits; gloo: the host does
+                    ctx = self._ctx_from(ctx_in, B, memory_shape)
+                pred = self.model.align_chunk(enc, num_overlap, ctx)
+                if i + 1 < n:
+                    sends.append(self._isend(pred, (i + 1) % W, keys))
+                mine[i] = self._summary(pred, len(chunks[i]))
+        for works, _ in sends:
+            for w in works:
+                w.wait()
+        if cuda:
+            main.wait_stream(side)
+            for v in mine.values():
+                _record_stream(v, main)
+        return mine
 
     def _gather(self, mine: Dict[int, dict], chunks: List[List[int]], num_overlap: int, B: int) -> Optional[dict]:
         n = len(chunks)

@@ -27,8 +27,13 @@ from ..utils.data import extri_to_pose_encoding, pose_encoding_to_extri
 from ..utils.geometry import averagePoseEncodings, closed_form_inverse_se3
 from ..utils.pose_enc import extri_intri_to_pose_encoding, pose_encoding_to_extri_intri
 
-# no-grad inference runs the per-chunk pose algebra on the host (see _align_chunk)
-_HOST_POSE = os.environ.get("VGGT_HOST_POSE", "1") != "0"
+# no-grad inference: the per-chunk pose / Sim(3) algebra of featureAligned_vggt.py:96-143
+# runs as ONE HIP launch (vggt_pose_compose, incl. the Markley eigen-average): no host
+# sync per chunk.  VGGT_POSE=host: the same fp32 torch algebra on the host after one
+# device-to-host copy (round-2 form); VGGT_POSE=device: torch ops on the device
+# (~300 small launches per chunk, profiles/r4w).  Training always takes the
+# differentiable torch form.
+_POSE_MODE = os.environ.get("VGGT_POSE", "hip")
 
 try:  # optional, as in the reference (featureAligned_vggt.py:3); only used for from_pretrained
     from huggingface_hub import PyTorchModelHubMixin
@@ -129,45 +134,19 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
 
         dev = images.device
         chunk_scale = chunk_sim3_enc[..., -1]  # on the device: depth / point scaling
-        # No-grad inference: the (B, S, 4, 4) quaternion / SE(3) algebra below runs on
-        # the host -- ~300 tiny elementwise launches per chunk on the device
-        # (profiles/r4w/align_chunk_ops.txt), and the Markley average already syncs
-        # on the host.  Same fp32 arithmetic; VGGT_HOST_POSE=0 keeps it on the device.
-        adev = torch.device("cpu") if (not train and _HOST_POSE and dev.type == "cuda") else dev
-        cs_a = chunk_sim3_enc.to(adev)
-        chunk_se3 = pose_encoding_to_extri(cs_a)
-        per_frame_se3 = torch.matmul(pose_encoding_to_extri(frame_se3_enc.to(adev)), chunk_se3)
-        per_frame_se3 = torch.cat([chunk_se3, per_frame_se3], dim=1)
-
-        point_identity_alignment = None
+        mode = "torch" if train or dev.type != "cuda" else _POSE_MODE
+        point_transform = None
         if self.camera_head is not None:
-            extr, intr = pose_encoding_to_extri_intri(enc["cam_pose_enc"].to(adev), image_size_hw=images.shape[-2:])
-            extr = F.pad(extr, (0, 0, 0, 1, 0, 0, 0, 0), mode="constant")
-            extr[:, :, 3, 3] = 1.0
-            ident = closed_form_inverse_se3(extr[:, 0])
-            point_identity_alignment = extr[:, 0].detach().clone()
-            extr = extr @ ident.view(B, 1, 4, 4)
-            extr[:, :, :3, 3] *= cs_a[..., -1].view(B, 1, 1)
-            if context is not None:
-                if gt_poses is not None:
-                    mean_camera_transform = gt_poses[:, :1].to(extr)
-                else:
-                    ctx_o = pose_encoding_to_extri(context["pose_enc"][-1][:, -overlap:].to(extr.device))
-                    inv_o = closed_form_inverse_se3(extr[:, :overlap].reshape(B * overlap, 4, 4)).reshape(
-                        B, overlap, 4, 4)
-                    ct = inv_o @ ctx_o
-                    if overlap > 1:
-                        mean_camera_transform = pose_encoding_to_extri(averagePoseEncodings(extri_to_pose_encoding(ct)))
-                    else:
-                        mean_camera_transform = ct
+            if mode == "hip":
+                ctx_pe = context["pose_enc"][-1] if context is not None else None
+                gt0 = gt_poses[:, 0] if (context is not None and gt_poses is not None) else None
+                aligned_pose_enc, point_transform = N.pose_compose(
+                    chunk_sim3_enc, frame_se3_enc, enc["cam_pose_enc"], ctx_pe, gt0, overlap, images.shape[-2:],
+                    want_point_transform=self.point_head is not None)
             else:
-                mean_camera_transform = torch.eye(4, device=adev, dtype=images.dtype).view(1, 1, 4, 4).expand(
-                    B, -1, -1, -1)
-            per_frame_se3 = torch.matmul(per_frame_se3, mean_camera_transform)
-            aligned_extr = torch.matmul(extr, per_frame_se3)
-            aligned_pose_enc = extri_intri_to_pose_encoding(aligned_extr, intr, image_size_hw=images.shape[-2:])
-            if adev != dev:
-                aligned_pose_enc = aligned_pose_enc.to(dev)
+                aligned_pose_enc, point_transform = self._compose_torch(
+                    enc, chunk_sim3_enc, frame_se3_enc, context, gt_poses, overlap, images,
+                    torch.device("cpu") if mode == "host" else dev)
 
             predictions["overlap_tokens"] = overlap_tokens
             if context is None:
@@ -204,22 +183,14 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
 
         if self.point_head is not None:
             pts3d, pts3d_conf = enc["points"], enc["points_conf"]
-            if adev != dev:
-                per_frame_se3 = per_frame_se3.to(dev)
-                if point_identity_alignment is not None:
-                    point_identity_alignment = point_identity_alignment.to(dev)
             if self.camera_head is not None:
-                if context is not None:
-                    pt = closed_form_inverse_se3(per_frame_se3[:, 0]).unsqueeze(1)
-                    pt = pt @ point_identity_alignment.view(B, 1, 4, 4)
-                else:
-                    pt = point_identity_alignment.view(B, 1, 4, 4)
+                pt = point_transform
                 if train:  # differentiable form (gradients into chunk_scale and pt)
                     pts3d = pts3d * chunk_scale.view(B, 1, 1, 1, 1)
                     pts3d = torch.einsum("bij,bshwj->bshwi", pt[:, 0, :3, :3], pts3d) + pt[:, 0, :3, 3].view(B, 1, 1, 1, 3)
                 else:
                     # featureAligned_vggt.py:200-206: scale, then the SE(3) of pt, one HIP pass
-                    pts3d = N.sim3_points(pts3d.contiguous(), pt[:, 0], chunk_scale.reshape(B))
+                    pts3d = N.sim3_points(pts3d.contiguous(), pt.reshape(B, 4, 4).to(dev), chunk_scale.reshape(B))
             if context is None:
                 predictions["world_points"] = [pts3d]
                 predictions["world_points_conf"] = [pts3d_conf]
@@ -236,6 +207,48 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
                 context.setdefault("images", []).append(images)
                 predictions["images"] = context["images"]
         return predictions
+
+    def _compose_torch(self, enc, chunk_sim3_enc, frame_se3_enc, context, gt_poses, overlap, images, adev):
+        """featureAligned_vggt.py:96-143 (+ the point transform of :187-196) as torch
+        ops on ``adev`` (training: differentiable on the device).  Returns the
+        aligned pose encoding (on the images' device) and the point transform
+        (B, 1, 4, 4)."""
+        B = images.shape[0]
+        dev = images.device
+        cs_a = chunk_sim3_enc.to(adev)
+        chunk_se3 = pose_encoding_to_extri(cs_a)
+        per_frame_se3 = torch.matmul(pose_encoding_to_extri(frame_se3_enc.to(adev)), chunk_se3)
+        per_frame_se3 = torch.cat([chunk_se3, per_frame_se3], dim=1)
+        extr, intr = pose_encoding_to_extri_intri(enc["cam_pose_enc"].to(adev), image_size_hw=images.shape[-2:])
+        extr = F.pad(extr, (0, 0, 0, 1, 0, 0, 0, 0), mode="constant")
+        extr[:, :, 3, 3] = 1.0
+        ident = closed_form_inverse_se3(extr[:, 0])
+        point_identity_alignment = extr[:, 0].detach().clone()
+        extr = extr @ ident.view(B, 1, 4, 4)
+        extr[:, :, :3, 3] *= cs_a[..., -1].view(B, 1, 1)
+        if context is not None:
+            if gt_poses is not None:
+                mean_camera_transform = gt_poses[:, :1].to(extr)
+            else:
+                ctx_o = pose_encoding_to_extri(context["pose_enc"][-1][:, -overlap:].to(extr.device))
+                inv_o = closed_form_inverse_se3(extr[:, :overlap].reshape(B * overlap, 4, 4)).reshape(
+                    B, overlap, 4, 4)
+                ct = inv_o @ ctx_o
+                if overlap > 1:
+                    mean_camera_transform = pose_encoding_to_extri(averagePoseEncodings(extri_to_pose_encoding(ct)))
+                else:
+                    mean_camera_transform = ct
+        else:
+            mean_camera_transform = torch.eye(4, device=adev, dtype=images.dtype).view(1, 1, 4, 4).expand(
+                B, -1, -1, -1)
+        per_frame_se3 = torch.matmul(per_frame_se3, mean_camera_transform)
+        aligned_extr = torch.matmul(extr, per_frame_se3)
+        aligned_pose_enc = extri_intri_to_pose_encoding(aligned_extr, intr, image_size_hw=images.shape[-2:])
+        if context is not None:
+            pt = closed_form_inverse_se3(per_frame_se3[:, 0]).unsqueeze(1) @ point_identity_alignment.view(B, 1, 4, 4)
+        else:
+            pt = point_identity_alignment.view(B, 1, 4, 4)
+        return aligned_pose_enc.to(dev), pt.to(dev)
 
 
 def merge_results(first_chunk, second_chunk, num_overlap: int = 0, mergeDim: int = 1):

@@ -56,9 +56,12 @@ def f32_param(mod: nn.Module, name: str, fill: Optional[float] = None, n: int = 
 
 
 class Workspace:
-    """Named, grow-only device buffers (one set per device)."""
+    """Named, grow-only device buffers: one set per (device, stream), so work
+    queued on two streams at once (the multi-GPU pipeline aligns chunk i on a
+    side stream while the compute stream encodes chunk i + W) never shares a
+    scratch buffer."""
 
-    _per_device: Dict[torch.device, "Workspace"] = {}
+    _per_device: Dict[tuple, "Workspace"] = {}
 
     def __init__(self, device):
         self.device = device
@@ -67,9 +70,15 @@ class Workspace:
     @classmethod
     def get(cls, device) -> "Workspace":
         device = torch.device(device)
-        ws = cls._per_device.get(device)
+        if device.type == "cuda":
+            if device.index is None:
+                device = torch.device("cuda", torch.cuda.current_device())
+            key = (device, torch.cuda.current_stream(device).stream_id)
+        else:
+            key = (device, 0)
+        ws = cls._per_device.get(key)
         if ws is None:
-            ws = cls._per_device[device] = Workspace(device)
+            ws = cls._per_device[key] = Workspace(device)
         return ws
 
     def buf(self, name: str, rows: int, cols: int, dtype=torch.float32) -> torch.Tensor:

@@ -642,6 +642,49 @@ def merge_results(first, second, num_overlap: int = 0, dim: int = 1):
     return torch.cat((first, second), dim=dim)
 
 
+def compose_poses(chunk_sim3: Tensor, frame_se3: Tensor, cam_pose_enc: Tensor, ctx_pose_enc: Optional[Tensor],
+                  gt_first: Optional[Tensor], overlap: int, hw) -> Tuple[Tensor, Tensor]:
+    """featureAligned_vggt.py:96-143 and the point transform of :187-196:
+    -> (aligned pose encoding (B,S,9), point transform (B,4,4)).
+    ctx_pose_enc = context["pose_enc"][-1] (None: first chunk); gt_first =
+    gt_poses[:, 0] (chunk_gt mode) or None."""
+    H, W = hw
+    B = cam_pose_enc.shape[0]
+    chunk_se3 = pose_encoding_to_extri(chunk_sim3)
+    chunk_scale = chunk_sim3[..., -1]
+    pf = pose_encoding_to_extri(frame_se3)
+    pf = torch.matmul(pf, chunk_se3)
+    pf = torch.cat([chunk_se3, pf], dim=1)
+    extr, intr = pose_encoding_to_extri_intri(cam_pose_enc, (H, W))
+    extr = F.pad(extr, (0, 0, 0, 1, 0, 0, 0, 0))
+    extr[:, :, 3, 3] = 1.0
+    ident = closed_form_inverse_se3(extr[:, 0])
+    pt_ident = extr[:, 0].clone()
+    extr = extr @ ident.view(B, 1, 4, 4)
+    extr[:, :, :3, 3] *= chunk_scale.view(B, 1, 1)
+    if ctx_pose_enc is not None:
+        if gt_first is not None:
+            mean_t = gt_first.reshape(B, 1, 4, 4).to(extr)
+        else:
+            ctx_o = pose_encoding_to_extri(ctx_pose_enc[:, -overlap:])
+            inv_o = closed_form_inverse_se3(extr[:, :overlap].reshape(B * overlap, 4, 4)).reshape(B, overlap, 4, 4)
+            ct = inv_o @ ctx_o
+            if overlap > 1:
+                mean_t = pose_encoding_to_extri(average_pose_encodings(extri_to_pose_encoding(ct)))
+            else:
+                mean_t = ct
+    else:
+        mean_t = torch.eye(4, dtype=cam_pose_enc.dtype).view(1, 1, 4, 4).expand(B, -1, -1, -1)
+    pf = torch.matmul(pf, mean_t)
+    aligned = torch.matmul(extr, pf)
+    aligned_enc = extri_intri_to_pose_encoding(aligned, intr, (H, W))
+    if ctx_pose_enc is not None:
+        tr = closed_form_inverse_se3(pf[:, 0]) @ pt_ident
+    else:
+        tr = pt_ident
+    return aligned_enc, tr
+
+
 def feature_aligned_encode(sd: SD, images: Tensor, enable_camera=True, enable_depth=True, enable_point=False,
                            bf16: bool = False, agg_kwargs: Optional[dict] = None) -> dict:
     """The context-free half of FeatureAlignedVGGT.forward: aggregator
@@ -686,36 +729,12 @@ def feature_aligned_compose(sd: SD, enc: dict, images: Tensor, num_overlap: int,
     overlap = num_overlap if S > num_overlap else S - 1
     chunk_sim3, frame_se3, mem, ov_tok = alignment_head(sd, toks[-1], (H, W), overlap, ctx_ov, ctx_mem,
                                                         num_memory_tokens=num_memory_tokens, bf16=bf16)
-    chunk_se3 = pose_encoding_to_extri(chunk_sim3)
     chunk_scale = chunk_sim3[..., -1]
-    pf = pose_encoding_to_extri(frame_se3)
-    pf = torch.matmul(pf, chunk_se3)
-    pf = torch.cat([chunk_se3, pf], dim=1)
     if enable_camera:
-        penc = enc["cam_pose_enc"]
-        extr, intr = pose_encoding_to_extri_intri(penc, (H, W))
-        extr = F.pad(extr, (0, 0, 0, 1, 0, 0, 0, 0))
-        extr[:, :, 3, 3] = 1.0
-        ident = closed_form_inverse_se3(extr[:, 0])
-        pt_ident = extr[:, 0].clone()
-        extr = extr @ ident.view(B, 1, 4, 4)
-        extr[:, :, :3, 3] *= chunk_scale.view(B, 1, 1)
-        if context is not None:
-            if gt_poses is not None:
-                mean_t = gt_poses[:, :1].to(extr)
-            else:
-                ctx_o = pose_encoding_to_extri(context["pose_enc"][-1][:, -overlap:])
-                inv_o = closed_form_inverse_se3(extr[:, :overlap].reshape(B * overlap, 4, 4)).reshape(B, overlap, 4, 4)
-                ct = inv_o @ ctx_o
-                if overlap > 1:
-                    mean_t = pose_encoding_to_extri(average_pose_encodings(extri_to_pose_encoding(ct)))
-                else:
-                    mean_t = ct
-        else:
-            mean_t = torch.eye(4, dtype=images.dtype).view(1, 1, 4, 4).expand(B, -1, -1, -1)
-        pf = torch.matmul(pf, mean_t)
-        aligned = torch.matmul(extr, pf)
-        aligned_enc = extri_intri_to_pose_encoding(aligned, intr, (H, W))
+        ctx_pe = context["pose_enc"][-1] if context is not None else None
+        aligned_enc, tr = compose_poses(chunk_sim3, frame_se3, enc["cam_pose_enc"], ctx_pe,
+                                        gt_poses[:, 0] if (context is not None and gt_poses is not None) else None,
+                                        overlap, (H, W))
         pred["overlap_tokens"] = ov_tok
         if context is None:
             pred["pose_enc"] = [aligned_enc]
@@ -744,13 +763,9 @@ def feature_aligned_compose(sd: SD, enc: dict, images: Tensor, num_overlap: int,
     if "points" in enc:
         pts, pconf = enc["points"], enc["points_conf"]
         if enable_camera:
-            if context is not None:
-                tr = closed_form_inverse_se3(pf[:, 0]).unsqueeze(1) @ pt_ident.view(B, 1, 4, 4)
-            else:
-                tr = pt_ident.view(B, 1, 4, 4)
             pts = pts * chunk_scale.view(B, 1, 1, 1, 1)
             ph = torch.cat([pts, torch.ones_like(pts[..., :1])], dim=-1).view(B, -1, 4)
-            pts = (ph @ tr[:, 0].transpose(-1, -2))[..., :3].view(B, S, H, W, 3)
+            pts = (ph @ tr.transpose(-1, -2))[..., :3].view(B, S, H, W, 3)
         if context is None:
             pred["world_points"], pred["world_points_conf"] = [pts], [pconf]
         else:

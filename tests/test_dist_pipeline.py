@@ -13,58 +13,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from aligned_vggt.dist.pipeline import ChunkPipeline, apply_sequence_to_model
-from aligned_vggt.models.featureAligned_vggt import merge_results
-
-P1, C, NMEM, DEC = 7, 16, 3, 8
-
-
-class ToyAlignModel:
-    """Same protocol as FeatureAlignedVGGT (encode_chunk / align_chunk /
-    forward + reference context semantics), tiny CPU arithmetic with a real
-    dependence on the previous chunk's overlap tokens, memory and poses."""
-
-    def encode_chunk(self, images):
-        B, S = images.shape[:2]
-        f = images.mean(dim=(2, 3, 4))  # (B, S)
-        tok = f[:, :, None, None] * torch.arange(1, P1 * C + 1, dtype=torch.float32).view(1, 1, P1, C) / 100
-        return {"images": images, "tok": tok, "depth": images[:, :, :1].permute(0, 1, 3, 4, 2) * 2,
-                "depth_conf": images[:, :, 1] + 1}
-
-    def align_chunk(self, enc, num_overlap, context=None):
-        tok = enc["tok"].clone()
-        B, S = tok.shape[:2]
-        ov = num_overlap if S > num_overlap else S - 1
-        if context is not None:
-            prev = context["overlap_tokens"]
-            tok = tok + prev.mean(dim=1, keepdim=True) * 0.5
-            mem = context["memory_tokens"][-1] * 0.9 + tok.mean() * 0.1
-            base = context["pose_enc"][-1][:, -ov:].mean(dim=1, keepdim=True)
-        else:
-            mem = torch.ones(B, NMEM, DEC)
-            base = torch.zeros(B, 1, 9)
-        pose = base + tok.mean(dim=(2, 3))[..., None] * torch.arange(9, dtype=torch.float32)
-        sim3 = tok.mean(dim=(1, 2, 3))[:, None, None].expand(B, 1, 8).clone()
-        fse3 = tok[:, 1:].mean(dim=(2, 3))[..., None].expand(B, S - 1, 7).clone()
-        scale = sim3[..., -1]
-        depth = enc["depth"] * scale.view(B, 1, 1, 1, 1)
-        pred = {"overlap_tokens": torch.cat([tok[:, :1], tok[:, -ov:]], 1).contiguous()}
-        if context is None:
-            pred.update(pose_enc=[pose], chunk_sim3_alignment_enc=sim3, frame_se3_alignment_enc=fse3,
-                        memory_tokens=[mem], depth=[depth], depth_conf=[enc["depth_conf"]])
-        else:
-            context.setdefault("pose_enc", []).append(pose)
-            pred["pose_enc"] = context["pose_enc"]
-            pred["chunk_sim3_alignment_enc"] = merge_results(context["chunk_sim3_alignment_enc"], sim3)
-            pred["frame_se3_alignment_enc"] = merge_results(context["frame_se3_alignment_enc"], fse3)
-            context.setdefault("memory_tokens", []).append(mem)
-            pred["memory_tokens"] = context["memory_tokens"]
-            for k, v in (("depth", depth), ("depth_conf", enc["depth_conf"])):
-                context.setdefault(k, []).append(v)
-                pred[k] = context[k]
-        return pred
-
-    def __call__(self, images, num_overlap, context=None, gt_poses=None):
-        return self.align_chunk(self.encode_chunk(images), num_overlap, context)
+from toy_model import C, DEC, NMEM, P1, ToyAlignModel
 
 
 def _free_port():
@@ -75,13 +24,13 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, Nf, w, ov, q):
+def _worker(rank, world, port, Nf, w, ov, q, group=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         g = torch.Generator().manual_seed(0)
         images = torch.rand(2, Nf, 3, 4, 5, generator=g)
-        out = ChunkPipeline(ToyAlignModel(), device=torch.device("cpu"), gather_dense=True).run(
+        out = ChunkPipeline(ToyAlignModel(), device=torch.device("cpu"), gather_dense=True, encode_group=group).run(
             images, w, ov, token_dims=(P1, C), memory_shape=(2, NMEM, DEC))
         if rank == 0:
             q.put({k: v.clone() for k, v in out.items()})
@@ -97,13 +46,17 @@ def _sequential(Nf, w, ov):
     return apply_sequence_to_model({"images": images}, ToyAlignModel(), [w, w], [ov, ov])
 
 
-@pytest.mark.parametrize("world,Nf,w,ov", [(2, 14, 5, 1), (2, 64, 16, 4), (3, 23, 6, 2), (4, 40, 8, 3)])
-def test_pipeline_matches_sequential_loop(world, Nf, w, ov):
+@pytest.mark.parametrize("world,Nf,w,ov,group", [(2, 14, 5, 1, None), (2, 64, 16, 4, None), (3, 23, 6, 2, None),
+                                                 (4, 40, 8, 3, None), (2, 44, 6, 2, 1), (2, 44, 6, 2, 2),
+                                                 (3, 60, 6, 2, 3)])
+def test_pipeline_matches_sequential_loop(world, Nf, w, ov, group):
+    """W ranks (isend/irecv baton ring, alignment on its own stream on GPUs),
+    incl. grouped encodes of each rank's own consecutive chunks."""
     ref = _sequential(Nf, w, ov)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, Nf, w, ov, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, Nf, w, ov, q, group)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)

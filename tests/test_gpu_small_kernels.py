@@ -206,3 +206,40 @@ def test_upsample_and_activate(N):
     ref = torch.sign(z[:, :3]) * torch.expm1(z[:, :3].abs()) * sc.repeat_interleave(50)[:, None]
     assert _rel(pts, ref) < 1e-6
     assert _rel(conf, 1 + z[:, 3].exp()) < 1e-6
+
+
+def _rand_quat(g, *shape):
+    """Unit quaternions spread over the whole sphere (every mat_to_quat branch)."""
+    return F.normalize(torch.randn(*shape, 4, generator=g), dim=-1)
+
+
+@pytest.mark.parametrize("B,S,S_prev,ov,mode", [(1, 16, 16, 4, "markley"), (2, 5, 5, 2, "markley"),
+                                                (3, 8, 16, 7, "markley"), (2, 6, 6, 1, "single"),
+                                                (2, 4, 4, 2, "gt"), (2, 9, 0, 0, "first"), (1, 1, 0, 0, "first")])
+def test_pose_compose_matches_oracle(N, B, S, S_prev, ov, mode):
+    """vggt_pose_compose (featureAligned_vggt.py:96-143, :187-196) against the
+    oracle's torch restatement: first chunk, Markley mean (ov > 1), single
+    overlap transform, chunk_gt; large rotations.  The Markley eigenvector's
+    sign is arbitrary but enters only through quat_to_mat, so outputs agree."""
+    from oracle import vggt_oracle as O
+    g = torch.Generator().manual_seed(B * 100 + S)
+    H, W = 154, 518
+    cs = torch.cat([torch.randn(B, 1, 3, generator=g), _rand_quat(g, B, 1), 0.5 + torch.rand(B, 1, 1, generator=g)], -1)
+    fs = torch.cat([torch.randn(B, S - 1, 3, generator=g), _rand_quat(g, B, S - 1) * 1.3], -1)
+    cam = torch.cat([torch.randn(B, S, 3, generator=g), _rand_quat(g, B, S) * 0.9,
+                     0.8 + 0.4 * torch.rand(B, S, 2, generator=g)], -1)
+    ctx = gt = None
+    if mode != "first":
+        ctx = torch.cat([torch.randn(B, S_prev, 3, generator=g), _rand_quat(g, B, S_prev),
+                         torch.rand(B, S_prev, 2, generator=g)], -1)
+    if mode == "gt":
+        gt = O.pose_encoding_to_extri(torch.cat([torch.randn(B, 1, 3, generator=g), _rand_quat(g, B, 1)], -1))[:, 0]
+    ref, ref_pt = O.compose_poses(cs, fs, cam, ctx, gt, ov, (H, W))
+    out, pt = N.pose_compose(cs.cuda(), fs.cuda(), cam.cuda(), ctx.cuda() if ctx is not None else None,
+                             gt.cuda() if gt is not None else None, ov, (H, W))
+    torch.cuda.synchronize()
+    out, pt = out.cpu(), pt.cpu()
+    assert _rel(out[..., :3], ref[..., :3]) < 2e-5, _rel(out[..., :3], ref[..., :3])
+    assert float((1 - (out[..., 3:7] * ref[..., 3:7]).sum(-1).abs()).abs().max()) < 1e-5  # w >= 0 in both
+    assert _rel(out[..., 7:], ref[..., 7:]) < 1e-6
+    assert _rel(pt, ref_pt) < 2e-5
