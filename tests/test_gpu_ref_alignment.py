@@ -5,8 +5,10 @@ shim; see tests/test_ref_alignment_golden.py for the oracle's pin).
 
 Tolerances (north star: Sim(3) within 1e-3 rel):
   * bf16 tier (trunk) vs the reference under emulated bf16-mixed autocast:
-    chunk Sim(3) < 1e-3; frame SE(3) / memory / overlap tokens < 2e-2 (the
-    reference's own bf16-vs-fp32 spread on these cases is ~1e-3);
+    chunk Sim(3) < 1e-3; frame SE(3) / memory / overlap tokens < 3e-3
+    (measured on MI355X: 3e-4 - 9e-4; the reference's own bf16-vs-fp32 spread
+    on these cases is ~7e-4 - 9e-4); composed poses / depths / points < 5e-3
+    (measured <= 1.7e-3 after four chained chunks), quaternions 1e-5, FoV 1e-6;
   * fp32 tier (decoder, cross-attention block in fp32) vs the fp32 reference:
     1e-5 rel.
 """
@@ -63,7 +65,7 @@ def test_alignment_head_vs_reference(heads, golden):
         print(case, "vs bf16 ref", e, "vs fp32 ref", e32)
         assert tuple(nov_t.shape) == g[f"{case}_bf16_new_ov"].shape
         assert e["chunk_sim3"] < 1e-3, (case, e)
-        assert max(e.values()) < 2e-2, (case, e)
+        assert max(e.values()) < 3e-3, (case, e)
 
 
 def test_decode_alignments_vs_reference(heads, golden):
@@ -120,7 +122,7 @@ def test_cross_attention_block_vs_reference(golden):
     got = xr[:G * S].view(G, S, 1024)
     e, e32 = _rel(got, g["tmp_bf16"]), _rel(got, g["tmp_f32"])
     print("temporal block vs bf16 ref", e, "vs fp32 ref", e32)
-    assert e < 2e-3, (e, e32)
+    assert e < 2e-4, (e, e32)  # measured 2.6e-5
 
 
 @pytest.fixture(scope="module")
@@ -180,5 +182,9 @@ def test_feature_aligned_composition_vs_reference(model, golden, run):
     for k, v in e.items():
         if k.startswith("fov"):
             assert v < 1e-6, (k, e)
+        elif k.startswith("q"):
+            assert v < 1e-5, (k, e)
+        elif k.startswith(("T", "depth", "pts")):
+            assert v < 5e-3, (k, e)
         else:
-            assert v < 2e-2, (k, e)
+            assert v < 3e-3, (k, e)
