@@ -274,6 +274,7 @@ def main():
                        "frames": args.frames, "tokens_per_chunk": args.frames * (5 + 37 * 37),
                        "parallelism": "replicas x%d" % world},
             "mfma_util_whole_step": round(fl["total"] * value / world / (PEAK_BF16_TFLOPS * 1e12), 4),
+            "mfma_util_pmc": _step_pmc(),
             "tflops_per_gpu": round(fl["total"] * value / world / 1e12, 1),
             "roofline": {"bound": "mfma", "kernel": "attn_fwd_kernel<64> (global attention, 1x16 heads x 21984^2 x 64)",
                          "achieved": round(attn_tflops, 1) if attn_tflops else None, "peak": PEAK_BF16_TFLOPS,
@@ -300,6 +301,24 @@ def _pmc_traffic():
             return json.load(fh)["hbm_bytes_per_launch"]
     except (OSError, ValueError, KeyError):
         return None
+
+
+def _step_pmc():
+    """Counter-based MFMA utilisation of the aggregator step from the committed
+    summary (profiles/step_mfma.json, scripts/gpu_step_pmc.sh: rocprofv3 --pmc
+    SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE over one step of this bench,
+    and SQ_INSTS_VALU_MFMA_MOPS_BF16), or None."""
+    p = os.path.join(ROOT, "profiles", "step_mfma.json")
+    try:
+        with open(p) as fh:
+            d = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    out = {"mfma_busy_frac": d.get("mfma_busy_frac"), "by_class": d.get("mfma_busy_frac_by_class"),
+           "source": "profiles/step_mfma.json"}
+    if d.get("mfma_bf16_tflop_counted") is not None:
+        out["bf16_tflop_counted_per_step"] = round(d["mfma_bf16_tflop_counted"], 3)
+    return out
 
 
 def bench_full(args, world, rank, dev):

@@ -309,6 +309,12 @@ int vggt_upsample_bilinear_f32(const float* x, int nimg, int hi, int wi, int C, 
 /* Same, writing y (f32, may be NULL) and/or the split bf16 halves of relu?(y) (contiguous [.., C]). */
 int vggt_upsample_bilinear_split(const float* x, int nimg, int hi, int wi, int C, float* y, int ho, int wo,
                                  const float* pos, void* y_hi, void* y_lo, int split_relu, void* stream);
+/* Same as vggt_upsample_bilinear_split with a SEPARABLE positional table (DPT's
+ * UV sin/cos embedding, dpt_head ext `_apply_pos_embed`: channels [0, C/2) depend on
+ * x only, [C/2, C) on y only): pos_sep = [wo + ho, C/2] fp32, rows 0..wo-1 the x
+ * part, rows wo..wo+ho-1 the y part.  C % 8 == 0. */
+int vggt_upsample_bilinear_split_sep(const float* x, int nimg, int hi, int wi, int C, float* y, int ho, int wo,
+                                     const float* pos_sep, void* y_hi, void* y_lo, int split_relu, void* stream);
 
 /*
  * DPT activate_head (ext): x [npix, ncl] NHWC with the confidence last;

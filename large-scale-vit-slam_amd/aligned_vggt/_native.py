@@ -55,6 +55,7 @@ _SIGS = {
     "vggt_conv2d_bf16x3_pre": [_vp, _vp, _i64, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _i64, _i, _vp,
                                _i64, _i, _vp, _i64, _vp, _i, _vp, _vp, _i64, _i, _vp],
     "vggt_upsample_bilinear_split": [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _i, _vp],
+    "vggt_upsample_bilinear_split_sep": [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _i, _vp],
     "vggt_split_act_bf16x2": [_vp, _i64, _i64, _i, _i, _vp, _vp, _vp],
     "vggt_upsample_bilinear_f32": [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp],
     "vggt_dpt_activate": [_vp, _i64, _i64, _i, _i, _i, _vp, _vp, _vp, _vp],
@@ -453,6 +454,17 @@ def upsample_bilinear_split(x: torch.Tensor, nimg: int, hi: int, wi: int, C: int
     rc = lib().vggt_upsample_bilinear_split(_p(x), nimg, hi, wi, C, _p(y), ho, wo, _p(pos), _p(yh), _p(yl),
                                             int(split_relu), _stream())
     _check(rc, "vggt_upsample_bilinear_split")
+
+
+def upsample_bilinear_split_sep(x: torch.Tensor, nimg: int, hi: int, wi: int, C: int, y, ho: int, wo: int,
+                                pos_sep: torch.Tensor, y_split=None, split_relu: bool = False):
+    """upsample_bilinear_split with the separable positional table [wo + ho, C/2]."""
+    _dev(x, "upsample_bilinear_split_sep")
+    yh, yl = y_split if y_split is not None else (None, None)
+    assert pos_sep.shape == (wo + ho, C // 2) and pos_sep.is_contiguous()
+    rc = lib().vggt_upsample_bilinear_split_sep(_p(x), nimg, hi, wi, C, _p(y), ho, wo, _p(pos_sep), _p(yh), _p(yl),
+                                                int(split_relu), _stream())
+    _check(rc, "vggt_upsample_bilinear_split_sep")
 
 
 def split_act_bf16x2(x: torch.Tensor, relu: bool = False, out=None):

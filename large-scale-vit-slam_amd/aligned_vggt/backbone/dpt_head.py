@@ -52,6 +52,17 @@ def pos_table(C: int, h: int, w: int, W_img: int, H_img: int, ratio: float = 0.1
     return (emb * ratio).contiguous()
 
 
+def pos_table_sep(C: int, h: int, w: int, W_img: int, H_img: int, ratio: float = 0.1) -> torch.Tensor:
+    """pos_table in separable form [w + h, C/2]: the first C/2 channels of the
+    embedding depend only on the pixel's u (x), the last C/2 only on v (y), so
+    rows 0..w-1 hold the x part and rows w..w+h-1 the y part -- the same
+    floats as pos_table's entries."""
+    grid = _uv_grid(w, h, W_img / H_img)  # (h, w, 2)
+    u = _make_sincos(C // 2, grid[0, :, 0])  # (w, C/2)
+    v = _make_sincos(C // 2, grid[:, 0, 1])  # (h, C/2)
+    return (torch.cat([u, v], 0) * ratio).contiguous()
+
+
 class ResidualConvUnit(nn.Module):
     def __init__(self, features, activation=None, bn=False, groups=1):
         super().__init__()
@@ -101,6 +112,13 @@ def _scratch(in_shape, out_shape) -> nn.Module:
 # split done in the conv's register-staged gather; bitwise equal) or "fp32"
 # (exact f32 MFMA).
 CONV_PRECISION = os.environ.get("VGGT_CONV", "bf16x3pre")
+
+# FeatureFusionBlock: run the 1x1 out_conv before the bilinear resize (the two
+# commute; see DPTHead._fuse); VGGT_DPT_REORDER=0 keeps the reference's order.
+REORDER_OUT_CONV = os.environ.get("VGGT_DPT_REORDER", "1") != "0"
+# final upsample: the positional table in separable [w + h, C/2] form (bitwise the
+# same values; VGGT_DPT_SEP_POS=0 reads the full [h*w, C] table per frame)
+SEPARABLE_POS = os.environ.get("VGGT_DPT_SEP_POS", "1") != "0"
 
 # The convolutions address their operands with 32-bit byte offsets
 # (conv.hip: VGGT_ERR_SHAPE at 2 GiB); a forward whose widest map reaches this
@@ -210,9 +228,12 @@ def _convT(x: _Map, conv: nn.ConvTranspose2d, f32=True, split=None) -> _Map:
     return _Map(y, x.n, x.h * k, x.w * k, co, ys, split == "relu")
 
 
-def _upsample(x: _Map, ho: int, wo: int, pos=None, f32=True, split=None) -> _Map:
+def _upsample(x: _Map, ho: int, wo: int, pos=None, f32=True, split=None, pos_sep=None) -> _Map:
     y, ys = _outputs(x.n * ho * wo, x.c, x.t.device, f32, split)
-    if ys is None:
+    if pos_sep is not None and ys is not None:
+        N.upsample_bilinear_split_sep(x.t, x.n, x.h, x.w, x.c, y, ho, wo, pos_sep, y_split=ys,
+                                      split_relu=split == "relu")
+    elif ys is None:
         N.upsample_bilinear_f32(x.t, x.n, x.h, x.w, x.c, y, ho, wo, pos)
     else:
         N.upsample_bilinear_split(x.t, x.n, x.h, x.w, x.c, y, ho, wo, pos, y_split=ys, split_relu=split == "relu")
@@ -257,11 +278,11 @@ class DPTHead(nn.Module):
             nn.Conv2d(features // 2, 32, kernel_size=3, stride=1, padding=1), nn.ReLU(inplace=True),
             nn.Conv2d(32, output_dim, kernel_size=1, stride=1, padding=0))
 
-    def _pos(self, C: int, h: int, w: int, W_img: int, H_img: int, device) -> torch.Tensor:
+    def _pos(self, C: int, h: int, w: int, W_img: int, H_img: int, device, sep: bool = False) -> torch.Tensor:
         cache = self.__dict__.setdefault("_mi355x_pos", {})
-        key = (C, h, w, W_img, H_img, str(device))
+        key = (C, h, w, W_img, H_img, str(device), sep)
         if key not in cache:
-            cache[key] = pos_table(C, h, w, W_img, H_img).to(device)
+            cache[key] = (pos_table_sep if sep else pos_table)(C, h, w, W_img, H_img).to(device)
         return cache[key]
 
     def _fuse(self, blk: FeatureFusionBlock, x0: _Map, x1: Optional[_Map], size, f32=True, split=None) -> _Map:
@@ -272,8 +293,17 @@ class DPTHead(nn.Module):
             t = _conv(x1, blk.resConfUnit1.conv1, relu_in=True, relu_out=True, f32=False, split="plain")
             out = _conv(t, blk.resConfUnit1.conv2, res1=x1, res1_relu=True, res2=x0, split="relu")
         t = _conv(out, blk.resConfUnit2.conv1, relu_in=True, relu_out=True, f32=False, split="plain")
-        out = _conv(t, blk.resConfUnit2.conv2, res1=out, res1_relu=True)
         ho, wo = size if size is not None else (out.h * 2, out.w * 2)
+        if REORDER_OUT_CONV:
+            # out_conv (1x1) before the bilinear resize instead of after: both are
+            # linear, the resize acts per channel with weights summing to 1
+            # (align_corners=True), so conv1x1(resize(x)) == resize(conv1x1(x)) in
+            # exact arithmetic (bias included) -- at the input resolution the 1x1
+            # conv touches 1/4 of the pixels (refinenet1: 148^2 instead of 296^2)
+            out = _conv(t, blk.resConfUnit2.conv2, res1=out, res1_relu=True, f32=False, split="plain")
+            y = _conv(out, blk.out_conv)
+            return _upsample(y, ho, wo, f32=f32, split=split)
+        out = _conv(t, blk.resConfUnit2.conv2, res1=out, res1_relu=True)
         up = _upsample(out, ho, wo, f32=False, split="plain")
         return _conv(up, blk.out_conv, f32=f32, split=split)
 
@@ -342,8 +372,11 @@ class DPTHead(nn.Module):
         out = self._fuse(sc.refinenet1, out, l1, None, f32=False, split="plain")
         out = _conv(out, sc.output_conv1)
         Ho, Wo = int(ph * self.patch_size / self.down_ratio), int(pw * self.patch_size / self.down_ratio)
-        out = _upsample(out, Ho, Wo, self._pos(out.c, Ho, Wo, W, H, dev) if self.pos_embed else None, f32=False,
-                        split="plain")
+        if self.pos_embed and _pre() and SEPARABLE_POS and out.c % 8 == 0:
+            out = _upsample(out, Ho, Wo, f32=False, split="plain", pos_sep=self._pos(out.c, Ho, Wo, W, H, dev, sep=True))
+        else:
+            out = _upsample(out, Ho, Wo, self._pos(out.c, Ho, Wo, W, H, dev) if self.pos_embed else None, f32=False,
+                            split="plain")
         out = _conv(out, sc.output_conv2[0], relu_out=True, f32=False, split="plain")
         out = _conv(out, sc.output_conv2[2])
         ncl = self.output_dim

@@ -655,11 +655,15 @@ __global__ __launch_bounds__(256) void split_bf16x2_kernel(const float* __restri
 }
 
 // Bilinear resize, align_corners=True, NHWC f32 (F.interpolate semantics),
-// optional positional table [ho*wo, C] added to the result.
+// optional positional table added to the result: [ho*wo, C] (pos_sep 0), or
+// separable (pos_sep 1: DPT's UV sin/cos embedding, whose first C/2 channels
+// depend on x only and the last C/2 on y only) as [wo + ho, C/2] = U rows
+// then V rows -- 1/ho of the full table's bytes, which the full form re-reads
+// for every frame (16 x 137 MB per 16-frame 518^2 chunk, profiles/r5c).
 __global__ __launch_bounds__(256) void upsample_kernel(const float* __restrict__ x, int nimg, int hi, int wi, int C,
                                                        float* __restrict__ y, int ho, int wo,
                                                        const float* __restrict__ pos, bf16_t* __restrict__ yh,
-                                                       bf16_t* __restrict__ yl, int split_relu) {
+                                                       bf16_t* __restrict__ yl, int split_relu, int pos_sep = 0) {
   const int c4n = C / 4;
   const int64_t total = (int64_t)nimg * ho * wo * c4n;
   const float sh = ho > 1 ? (float)(hi - 1) / (float)(ho - 1) : 0.f;
@@ -681,7 +685,14 @@ __global__ __launch_bounds__(256) void upsample_kernel(const float* __restrict__
     const f32x4 v10 = *(const f32x4*)(b + ((int64_t)y1 * wi + x0) * C + c);
     const f32x4 v11 = *(const f32x4*)(b + ((int64_t)y1 * wi + x1) * C + c);
     f32x4 o = hy * (hx * v00 + lx * v01) + ly * (hx * v10 + lx * v11);
-    if (pos) o += *(const f32x4*)(pos + (int64_t)rem * C + c);
+    if (pos) {
+      if (pos_sep) {
+        const int hc = C / 2;
+        o += c < hc ? *(const f32x4*)(pos + (int64_t)ox * hc + c) : *(const f32x4*)(pos + (int64_t)(wo + oy) * hc + c - hc);
+      } else {
+        o += *(const f32x4*)(pos + (int64_t)rem * C + c);
+      }
+    }
     if (y) *(f32x4*)(y + p * C + c) = o;
     if (yh) {
       float h[4];
@@ -890,6 +901,19 @@ extern "C" int vggt_upsample_bilinear_split(const float* x, int nimg, int hi, in
   if (((uintptr_t)x | (uintptr_t)y) % 16 || ((uintptr_t)y_hi | (uintptr_t)y_lo) % 8) return VGGT_ERR_ALIGN;
   upsample_kernel<<<grid_for((int64_t)nimg * ho * wo * (C / 4)), 256, 0, (hipStream_t)stream>>>(
       x, nimg, hi, wi, C, y, ho, wo, pos, (bf16_t*)y_hi, (bf16_t*)y_lo, split_relu);
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+extern "C" int vggt_upsample_bilinear_split_sep(const float* x, int nimg, int hi, int wi, int C, float* y, int ho,
+                                                int wo, const float* pos_sep, void* y_hi, void* y_lo, int split_relu,
+                                                void* stream) {
+  if (nimg <= 0 || hi <= 0 || wi <= 0 || ho <= 0 || wo <= 0 || C % 8 || (!y && !y_hi) || (!y_hi != !y_lo) || !pos_sep)
+    return VGGT_ERR_SHAPE;
+  if (((uintptr_t)x | (uintptr_t)y | (uintptr_t)pos_sep) % 16 || ((uintptr_t)y_hi | (uintptr_t)y_lo) % 8)
+    return VGGT_ERR_ALIGN;
+  upsample_kernel<<<grid_for((int64_t)nimg * ho * wo * (C / 4)), 256, 0, (hipStream_t)stream>>>(
+      x, nimg, hi, wi, C, y, ho, wo, pos_sep, (bf16_t*)y_hi, (bf16_t*)y_lo, split_relu, 1);
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
 }

@@ -1,0 +1,114 @@
+"""Oracle parity at the production shapes (reduced depth), where the code
+paths that only switch on at size run composed:
+
+  * the headline chunk, 1 x 16 x 518^2 (BASELINE configs[1]): 21,984 token
+    rows -> 8-wave global attention, persistent GEMMs with the fused q/k-norm +
+    RoPE and GELU epilogues, the fused residual-add + next-LayerNorm row pass;
+  * the VKitti-shaped 154 x 518 sequence chunk (configs[3]/[4]: 16 frames,
+    overlap 4, 6,592 token rows) through apply_sequence_to_model with a shorter
+    tail chunk (featureAligned_vggt.py:93, data.py:188-190), memory on.
+
+The CPU oracle runs the same reduced depth (~20-60 s on the box's cores)."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from oracle import vggt_oracle as O  # noqa: E402
+
+
+def _rel(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.fixture(scope="module")
+def cuda():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    return torch.device("cuda")
+
+
+def test_aggregator_headline_chunk_reduced_depth(cuda):
+    """Aggregator(depth=2, dino_depth=1) on one 16 x 518^2 chunk vs the oracle's
+    bf16-mixed emulation (same tolerance as the small-shape tests)."""
+    from aligned_vggt.backbone.aggregator import Aggregator
+    from aligned_vggt.utils.synthetic import synthetic_images, synthetic_init_
+    agg = Aggregator(depth=2, dino_depth=1)
+    synthetic_init_(agg, seed=7)
+    sd = {"aggregator." + k: v for k, v in agg.state_dict().items()}
+    img = synthetic_images(1, 16, 518, 518, seed=1234)
+    agg = agg.to(cuda)
+    outs, psi = agg(img.to(cuda), keep_layers=(0, 1))
+    torch.cuda.synchronize()
+    outs = [o.cpu() for o in outs]
+    with torch.no_grad():
+        ref, psi_ref = O.aggregator(sd, img, bf16=True, keep=(0, 1), depth=2, dino_depth=1)
+    assert psi == psi_ref == 5
+    for o, r in zip(outs, ref):
+        assert o.shape == r.shape == (1, 16, 1374, 2048)
+        assert torch.isfinite(o).all()
+        e = _rel(o, r)
+        print("headline chunk layer rel-L2 vs bf16 oracle", e)
+        assert e < 2e-2, e
+
+
+def test_vkitti_sequence_with_tail_reduced_depth(cuda, monkeypatch):
+    """36 frames of 154 x 518, chunk 16 / overlap 4 -> chunks [0-15], [12-27] and
+    a 12-frame tail [24-35]: HIP model through apply_sequence_to_model (grouped
+    encode of the two equal chunks, the tail alone) vs the oracle chunk loop."""
+    from aligned_vggt.backbone.aggregator import Aggregator
+    from aligned_vggt.dist.pipeline import apply_sequence_to_model
+    from aligned_vggt.models.featureAligned_vggt import FeatureAlignedVGGT
+    from aligned_vggt.utils.synthetic import condition_pose_outputs_, synthetic_images, synthetic_init_
+    N, w, ov, H, W = 36, 16, 4, 154, 518
+    chunks = O.generate_chunks(N, w, ov)
+    assert [len(c) for c in chunks] == [16, 16, 12]
+    from aligned_vggt.models import featureAligned_vggt as FAmod
+    monkeypatch.setattr(FAmod, "Aggregator", lambda **kw: Aggregator(depth=4, dino_depth=1, **kw))
+    m = FeatureAlignedVGGT(enable_point=False, enable_track=False, num_memory_tokens=8)
+    m.intermediate_layer_indices = [0, 1, 2, 3]
+    synthetic_init_(m, seed=13)
+    condition_pose_outputs_(m)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(cuda).eval()
+    imgs = synthetic_images(1, N, H, W, seed=31)
+    got = apply_sequence_to_model({"images": imgs.to(cuda)}, m, [w], [ov], "chunk_overlap", None)
+    torch.cuda.synchronize()
+    agg_kw = {"keep": (0, 1, 2, 3), "depth": 4, "dino_depth": 1}
+
+    def oracle(bf16):
+        ctx = None
+        with torch.no_grad():
+            for ids in chunks:
+                ctx = O.feature_aligned_forward(sd, imgs[:, ids], ov, ctx, bf16=bf16, agg_kwargs=agg_kw)
+        return ctx
+
+    ref, ref32 = oracle(True), oracle(False)
+    pe_ref = torch.cat([p[:, (ov if i else 0):] for i, p in enumerate(ref["pose_enc"])], 1)
+    pe_32 = torch.cat([p[:, (ov if i else 0):] for i, p in enumerate(ref32["pose_enc"])], 1)
+    d_ref = torch.cat([d[:, (ov if i else 0):] for i, d in enumerate(ref["depth"])], 1)
+    e = {"chunk_sim3": _rel(got["chunk_sim3_alignment_enc"], ref["chunk_sim3_alignment_enc"]),
+         "frame_se3": _rel(got["frame_se3_alignment_enc"], ref["frame_se3_alignment_enc"]),
+         "pose_T": _rel(got["pose_enc"][..., :3], pe_ref[..., :3]),
+         "pose_fov": _rel(got["pose_enc"][..., 7:], pe_ref[..., 7:]),
+         "depth": _rel(got["depth"], d_ref)}
+    d_32 = torch.cat([d[:, (ov if i else 0):] for i, d in enumerate(ref32["depth"])], 1)
+    e_ref = {"chunk_sim3": _rel(ref32["chunk_sim3_alignment_enc"], ref["chunk_sim3_alignment_enc"]),
+             "frame_se3": _rel(ref32["frame_se3_alignment_enc"], ref["frame_se3_alignment_enc"]),
+             "pose_T": _rel(pe_32[..., :3], pe_ref[..., :3]), "pose_fov": _rel(pe_32[..., 7:], pe_ref[..., 7:]),
+             "depth": _rel(d_32, d_ref)}
+    print("154x518 sequence: hip vs bf16 oracle", e, "oracle fp32 vs bf16", e_ref)
+    assert got["pose_enc"].shape == (1, N, 9) and got["depth"].shape[:2] == (1, N)
+    assert got["chunk_sim3_alignment_enc"].shape == (1, 3, 8)
+    # north star on the Sim(3) chunk alignment; the rest through the random-init
+    # camera head / decoders, which amplify bf16 token rounding chaotically (the
+    # oracle's own bf16-vs-fp32 spread here: pose T ~6e-2, FoV ~3e-2): within 3e-2
+    # of the bf16 emulation or no further than twice that spread (as
+    # test_gpu_model.py's two-chunk test)
+    assert e["chunk_sim3"] < 1e-3, e
+    for k in ("frame_se3", "pose_T", "pose_fov", "depth"):
+        assert e[k] < 3e-2 or e[k] < 2.0 * e_ref[k], (k, e, e_ref)

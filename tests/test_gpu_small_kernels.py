@@ -243,3 +243,26 @@ def test_pose_compose_matches_oracle(N, B, S, S_prev, ov, mode):
     assert float((1 - (out[..., 3:7] * ref[..., 3:7]).sum(-1).abs()).abs().max()) < 1e-5  # w >= 0 in both
     assert _rel(out[..., 7:], ref[..., 7:]) < 1e-6
     assert _rel(pt, ref_pt) < 2e-5
+
+
+def test_upsample_separable_pos_bitwise(N):
+    """The final DPT upsample with the separable [w + h, C/2] positional table
+    equals the full [h*w, C] table form bitwise (same floats, same adds)."""
+    from aligned_vggt.backbone.dpt_head import pos_table, pos_table_sep
+    n, hi, wi, C, ho, wo = 2, 9, 13, 16, 22, 31
+    x = torch.randn(n * hi * wi, C, device="cuda")
+    full = pos_table(C, ho, wo, wo, ho).cuda()
+    sep = pos_table_sep(C, ho, wo, wo, ho).cuda()
+    outs = []
+    for kind in ("full", "sep"):
+        y = torch.empty(n * ho * wo, C, device="cuda")
+        ys = (torch.empty(n * ho * wo, C, device="cuda", dtype=torch.bfloat16),
+              torch.empty(n * ho * wo, C, device="cuda", dtype=torch.bfloat16))
+        if kind == "full":
+            N.upsample_bilinear_split(x, n, hi, wi, C, y, ho, wo, full, y_split=ys)
+        else:
+            N.upsample_bilinear_split_sep(x, n, hi, wi, C, y, ho, wo, sep, y_split=ys)
+        outs.append((y, ys))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1][0], outs[1][1][0]) and torch.equal(outs[0][1][1], outs[1][1][1])
