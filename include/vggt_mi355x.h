@@ -317,6 +317,22 @@ int vggt_upsample_bilinear_split_sep(const float* x, int nimg, int hi, int wi, i
                                      const float* pos_sep, void* y_hi, void* y_lo, int split_relu, void* stream);
 
 /*
+ * Fused last stage of the DPT head (output_conv1's output -> F.interpolate(size=(ho, wo),
+ * bilinear, align_corners=True) -> + _apply_pos_embed -> output_conv2[0], dpt_head ext,
+ * featureAligned_vggt.py:166): y = conv3x3_pad1(split(resize(x) + pos)) without
+ * materialising the resized map.  x [nimg, hi, wi, C] f32 NHWC (C % 32 == 0), pos_sep
+ * [wo + ho, C/2] (the separable table of vggt_upsample_bilinear_split_sep) or NULL,
+ * w_hi / w_lo the split packed weights of vggt_conv2d_bf16x3_pre ([>= 32 rows, 9*C], the
+ * (ky, kx, ci) column order), co <= 32.  Outputs as conv2d_bf16x3_pre: y [nimg*ho*wo, ldy]
+ * f32 and/or the split halves of relu?(y).  Same products and K order as the unfused
+ * upsample + conv2d_bf16x3_pre.
+ */
+int vggt_conv2d_upsample_bf16x3(const float* x, int nimg, int hi, int wi, int C, const float* pos_sep, int ho,
+                                int wo, const void* w_hi, const void* w_lo, const float* bias, int co, int relu_out,
+                                float* y, int64_t ldy, void* y_hi, void* y_lo, int64_t ldys, int split_relu,
+                                void* stream);
+
+/*
  * DPT activate_head (ext): x [npix, ncl] NHWC with the confidence last;
  * pts[p, j] = act(x[p, j]) * scale[p / pix_per_img]  (act 0 = exp, 1 = inv_log),
  * conf[p] = 1 + exp(x[p, ncl-1]) (expp1).  scale may be NULL (depth *= chunk

@@ -56,6 +56,8 @@ _SIGS = {
                                _i64, _i, _vp, _i64, _vp, _i, _vp, _vp, _i64, _i, _vp],
     "vggt_upsample_bilinear_split": [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _i, _vp],
     "vggt_upsample_bilinear_split_sep": [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _i, _vp],
+    "vggt_conv2d_upsample_bf16x3": [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _i, _i, _vp, _i64, _vp, _vp,
+                                    _i64, _i, _vp],
     "vggt_split_act_bf16x2": [_vp, _i64, _i64, _i, _i, _vp, _vp, _vp],
     "vggt_upsample_bilinear_f32": [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp],
     "vggt_dpt_activate": [_vp, _i64, _i64, _i, _i, _i, _vp, _vp, _vp, _vp],
@@ -465,6 +467,19 @@ def upsample_bilinear_split_sep(x: torch.Tensor, nimg: int, hi: int, wi: int, C:
     rc = lib().vggt_upsample_bilinear_split_sep(_p(x), nimg, hi, wi, C, _p(y), ho, wo, _p(pos_sep), _p(yh), _p(yl),
                                                 int(split_relu), _stream())
     _check(rc, "vggt_upsample_bilinear_split_sep")
+
+
+def conv2d_upsample_bf16x3(x: torch.Tensor, nimg: int, hi: int, wi: int, C: int, pos_sep: Optional[torch.Tensor],
+                           ho: int, wo: int, w_hi: torch.Tensor, w_lo: torch.Tensor, bias, co: int,
+                           y: Optional[torch.Tensor], relu_out: bool = False, y_split=None, split_relu: bool = False):
+    """3x3 conv (pad 1) of the bilinear resize (align_corners) of x [nimg*hi*wi, C] to (ho, wo)
+    plus the separable positional table, on split-bf16 operands, without the resized map."""
+    _dev(x, "conv2d_upsample_bf16x3")
+    yh, yl = y_split if y_split is not None else (None, None)
+    rc = lib().vggt_conv2d_upsample_bf16x3(_p(x), nimg, hi, wi, C, _p(pos_sep), ho, wo, _p(w_hi), _p(w_lo), _p(bias),
+                                           co, int(relu_out), _p(y), _ld(y) if y is not None else 0, _p(yh), _p(yl),
+                                           _ld(yh) if yh is not None else 0, int(split_relu), _stream())
+    _check(rc, "vggt_conv2d_upsample_bf16x3")
 
 
 def split_act_bf16x2(x: torch.Tensor, relu: bool = False, out=None):

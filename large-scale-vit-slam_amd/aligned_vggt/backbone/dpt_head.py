@@ -119,6 +119,10 @@ REORDER_OUT_CONV = os.environ.get("VGGT_DPT_REORDER", "1") != "0"
 # final upsample: the positional table in separable [w + h, C/2] form (bitwise the
 # same values; VGGT_DPT_SEP_POS=0 reads the full [h*w, C] table per frame)
 SEPARABLE_POS = os.environ.get("VGGT_DPT_SEP_POS", "1") != "0"
+# output_conv1 -> resize -> + pos -> output_conv2[0] as one fused launch
+# (vggt_conv2d_upsample_bf16x3: the resized 518^2 map is never written);
+# VGGT_DPT_FUSE_UP=0 runs the separate upsample + conv
+FUSE_UPSAMPLE_CONV = os.environ.get("VGGT_DPT_FUSE_UP", "1") != "0"
 
 # The convolutions address their operands with 32-bit byte offsets
 # (conv.hip: VGGT_ERR_SHAPE at 2 GiB); a forward whose widest map reaches this
@@ -238,6 +242,17 @@ def _upsample(x: _Map, ho: int, wo: int, pos=None, f32=True, split=None, pos_sep
     else:
         N.upsample_bilinear_split(x.t, x.n, x.h, x.w, x.c, y, ho, wo, pos, y_split=ys, split_relu=split == "relu")
     return _Map(y, x.n, ho, wo, x.c, ys, split == "relu")
+
+
+def _conv_upsample(x: _Map, conv: nn.Conv2d, ho: int, wo: int, pos_sep, relu_out=False, f32=True, split=None) -> _Map:
+    """conv3x3(resize(x) + pos) as one launch (vggt_conv2d_upsample_bf16x3): x's f32 rows
+    at the source resolution, the resized map never materialised."""
+    _, b, w_hi, w_lo = _pack_conv(conv)
+    co = conv.weight.shape[0]
+    y, ys = _outputs(x.n * ho * wo, co, x.t.device, f32, split)
+    N.conv2d_upsample_bf16x3(x.t, x.n, x.h, x.w, x.c, pos_sep, ho, wo, w_hi, w_lo, b, co, y, relu_out=relu_out,
+                             y_split=ys, split_relu=split == "relu")
+    return _Map(y, x.n, ho, wo, co, ys, split == "relu")
 
 
 class DPTHead(nn.Module):
@@ -372,12 +387,19 @@ class DPTHead(nn.Module):
         out = self._fuse(sc.refinenet1, out, l1, None, f32=False, split="plain")
         out = _conv(out, sc.output_conv1)
         Ho, Wo = int(ph * self.patch_size / self.down_ratio), int(pw * self.patch_size / self.down_ratio)
-        if self.pos_embed and _pre() and SEPARABLE_POS and out.c % 8 == 0:
-            out = _upsample(out, Ho, Wo, f32=False, split="plain", pos_sep=self._pos(out.c, Ho, Wo, W, H, dev, sep=True))
+        c2 = sc.output_conv2[0]
+        if (FUSE_UPSAMPLE_CONV and _pre() and self.pos_embed and out.c % 32 == 0 and c2.weight.shape[0] <= 32
+                and c2.kernel_size == (3, 3) and c2.padding == (1, 1) and c2.stride == (1, 1)):
+            out = _conv_upsample(out, c2, Ho, Wo, self._pos(out.c, Ho, Wo, W, H, dev, sep=True), relu_out=True,
+                                 f32=False, split="plain")
         else:
-            out = _upsample(out, Ho, Wo, self._pos(out.c, Ho, Wo, W, H, dev) if self.pos_embed else None, f32=False,
-                            split="plain")
-        out = _conv(out, sc.output_conv2[0], relu_out=True, f32=False, split="plain")
+            if self.pos_embed and _pre() and SEPARABLE_POS and out.c % 8 == 0:
+                out = _upsample(out, Ho, Wo, f32=False, split="plain",
+                                pos_sep=self._pos(out.c, Ho, Wo, W, H, dev, sep=True))
+            else:
+                out = _upsample(out, Ho, Wo, self._pos(out.c, Ho, Wo, W, H, dev) if self.pos_embed else None,
+                                f32=False, split="plain")
+            out = _conv(out, c2, relu_out=True, f32=False, split="plain")
         out = _conv(out, sc.output_conv2[2])
         ncl = self.output_dim
         npix = F_ * Ho * Wo

@@ -60,6 +60,22 @@ def main():
         mb = (n * hi * hi * C * 4 + n * ho * ho * C * 4 + ho * ho * C * 4) / 1e6
         print(f"up: upsample 296->518 x{C} (+pos, split out): {us:.1f} us  {mb / us:.2f} TB/s algorithmic "
               f"({mb:.0f} MB)", flush=True)
+    if not a.only or "fused" in a.only:
+        from aligned_vggt.backbone.dpt_head import pos_table_sep
+        n, hi, C, ho, co = 16, 296, 128, 518, 32
+        x = torch.randn(n * hi * hi, C, device=dev, generator=g)
+        sep = pos_table_sep(C, ho, ho, ho, ho).to(dev)
+        wp = torch.zeros(128, 9 * C, device=dev)
+        wp[:co] = torch.randn(co, 9 * C, device=dev, generator=g) * 0.02
+        whi, wlo = N.split_bf16x2(wp)
+        b = torch.zeros(co, device=dev)
+        ys = (torch.empty(n * ho * ho, co, device=dev, dtype=torch.bfloat16),
+              torch.empty(n * ho * ho, co, device=dev, dtype=torch.bfloat16))
+        us = timeit(lambda: N.conv2d_upsample_bf16x3(x, n, hi, hi, C, sep, ho, ho, whi, wlo, b, co, None,
+                                                     relu_out=True, y_split=ys), a.reps)
+        fl = 2 * n * ho * ho * co * 9 * C
+        print(f"fused: upsample 296->518 + conv3x3 {C}->{co}: {us:.1f} us  bf16 MFMA {3 * fl / us / 1e6:.0f} TF/s",
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -37,7 +37,8 @@ def main():
                 "reordered": {"REORDER_OUT_CONV": True, "SEPARABLE_POS": False},
                 "reordered+sep_pos": {"REORDER_OUT_CONV": True, "SEPARABLE_POS": True}}
     if hasattr(D, "FUSE_UPSAMPLE_CONV"):
-        variants["reordered+fused_up"] = {"REORDER_OUT_CONV": True, "FUSE_UPSAMPLE_CONV": True}
+        variants["reordered+sep_pos+fused_up"] = {"REORDER_OUT_CONV": True, "SEPARABLE_POS": True,
+                                                  "FUSE_UPSAMPLE_CONV": True}
         for v in variants.values():
             v.setdefault("FUSE_UPSAMPLE_CONV", False)
     outs, times = {}, {k: [] for k in variants}

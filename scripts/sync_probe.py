@@ -36,6 +36,8 @@ sites = collections.Counter()
 def show(message, category, filename, lineno, file=None, line=None):
     st = [f for f in traceback.extract_stack() if "aligned_vggt" in f.filename]
     key = " <- ".join(f"{os.path.basename(f.filename)}:{f.lineno}:{f.name}" for f in reversed(st[-3:]))
+    if "prototype feature" in str(message):  # the mode's own notice, not a sync
+        return
     sites[(str(message)[:60], key)] += 1
 
 

@@ -266,3 +266,42 @@ def test_upsample_separable_pos_bitwise(N):
     torch.cuda.synchronize()
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1][0], outs[1][1][0]) and torch.equal(outs[0][1][1], outs[1][1][1])
+
+
+@pytest.mark.parametrize("n,hi,wi,C,ho,wo,co", [(2, 9, 13, 64, 22, 37, 32), (1, 17, 17, 128, 30, 30, 17),
+                                                (3, 8, 6, 32, 8, 6, 32), (16, 74, 74, 128, 130, 130, 32)])
+def test_conv_upsample_fused(N, n, hi, wi, C, ho, wo, co):
+    """vggt_conv2d_upsample_bf16x3 (resize + separable pos + split + 3x3 conv in one
+    launch) against the unfused upsample_split_sep + conv2d_bf16x3_pre (same
+    products: equal to fp32 round-off) and against torch fp32 (F.interpolate,
+    align_corners=True, + pos, F.conv2d) at the split-bf16 tolerance; ragged
+    4 x 32 output tiles at the image edges, co < 32."""
+    from aligned_vggt.backbone.dpt_head import pos_table, pos_table_sep
+    g = torch.Generator(device="cuda").manual_seed(n * 1000 + ho)
+    x = torch.randn(n * hi * wi, C, device="cuda", generator=g)
+    w = torch.randn(co, C, 3, 3, device="cuda", generator=g) * 0.05
+    b = torch.randn(co, device="cuda", generator=g) * 0.1
+    wp = torch.zeros(128, 9 * C, device="cuda")
+    wp[:co] = w.permute(0, 2, 3, 1).reshape(co, 9 * C)
+    whi, wlo = N.split_bf16x2(wp)
+    sep = pos_table_sep(C, ho, wo, wo, ho).cuda()
+    y = torch.empty(n * ho * wo, co, device="cuda")
+    ys = (torch.empty(n * ho * wo, co, device="cuda", dtype=torch.bfloat16),
+          torch.empty(n * ho * wo, co, device="cuda", dtype=torch.bfloat16))
+    N.conv2d_upsample_bf16x3(x, n, hi, wi, C, sep, ho, wo, whi, wlo, b, co, y, relu_out=True, y_split=ys)
+    # unfused form
+    uh = torch.empty(n * ho * wo, C, device="cuda", dtype=torch.bfloat16)
+    ul = torch.empty_like(uh)
+    N.upsample_bilinear_split_sep(x, n, hi, wi, C, None, ho, wo, sep, y_split=(uh, ul))
+    y2 = torch.empty_like(y)
+    N.conv2d_bf16x3_pre(uh, ul, n, ho, wo, C, whi, wlo, b, co, 3, 3, 1, 1, y2, relu_out=True)
+    # torch fp32
+    xi = x.view(n, hi, wi, C).permute(0, 3, 1, 2)
+    up = F.interpolate(xi, size=(ho, wo), mode="bilinear", align_corners=True)
+    up = up + pos_table(C, ho, wo, wo, ho).cuda().view(ho, wo, C).permute(2, 0, 1)[None]
+    ref = F.relu(F.conv2d(up, w, b, padding=1)).permute(0, 2, 3, 1).reshape(-1, co)
+    torch.cuda.synchronize()
+    assert _rel(y, y2) < 1e-6, _rel(y, y2)
+    assert _rel(y, ref) < 3e-5, _rel(y, ref)
+    hv = y.to(torch.bfloat16)
+    assert torch.equal(ys[0], hv) and _rel(ys[0].float() + ys[1].float(), y) < 1e-5
