@@ -110,23 +110,30 @@ def test_heads_fp32_tier_tight(models):
 
 def test_dpt_presplit_bitwise(models):
     """The pre-split DPT path (each producer writes the split halves its consumer
-    gathers) is bitwise equal to the register-staged split form."""
+    gathers) is bitwise equal to the register-staged split form; the fused
+    output stage agrees to fp32 round-off."""
     m, sd = models
     from aligned_vggt.backbone import dpt_head as D
     from aligned_vggt.utils.synthetic import synthetic_images
     imgs = synthetic_images(1, 2, 56, 70, seed=4)
     toks, psi = O.aggregator(sd, imgs, bf16=True)
     tg = [t.cuda() for t in toks]
-    prev = D.CONV_PRECISION
+    prev = D.CONV_PRECISION, D.FUSE_UPSAMPLE_CONV
     try:
         outs = {}
+        D.FUSE_UPSAMPLE_CONV = False
         for prec in ("bf16x3", "bf16x3pre"):
             D.CONV_PRECISION = prec
             outs[prec] = m.depth_head(tg, images=imgs.cuda(), patch_start_idx=psi)
+        # the fused resize + conv output stage (vggt_conv2d_upsample_bf16x3): same
+        # products, its interpolation compiled in another kernel -> fp32 round-off
+        D.FUSE_UPSAMPLE_CONV = True
+        outs["fused"] = m.depth_head(tg, images=imgs.cuda(), patch_start_idx=psi)
     finally:
-        D.CONV_PRECISION = prev
+        D.CONV_PRECISION, D.FUSE_UPSAMPLE_CONV = prev
     assert torch.equal(outs["bf16x3"][0], outs["bf16x3pre"][0])
     assert torch.equal(outs["bf16x3"][1], outs["bf16x3pre"][1])
+    assert _rel(outs["fused"][0], outs["bf16x3pre"][0]) < 1e-6 and _rel(outs["fused"][1], outs["bf16x3pre"][1]) < 1e-6
 
 
 def test_dpt_frame_groups_match(models, monkeypatch):
