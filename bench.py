@@ -416,12 +416,25 @@ def bench_train(args, world, rank, dev):
     wcs = torch.randn(1, 1, 8, device=dev, generator=g)
     wfs = torch.randn(1, S - 1, 7, device=dev, generator=g)
 
-    def step():
+    def fwd_bwd():
         cs1, fs1, m1, o1 = head(toks[0], (H, W), ov)
         cs2, fs2, m2, _ = head(toks[1], (H, W), ov, overlap_tokens=o1, memory_tokens=m1)
         loss = ((cs1 + cs2) * wcs).sum() + ((fs1 + fs2) * wfs).sum() + m2.square().sum()
         opt.zero_grad(set_to_none=True)
         loss.backward()
+        return loss
+
+    # VGGT_TRAIN_GRAPH=1: the ~2,000-launch forward + backward as one HIP graph
+    # (runtime.GraphedStep; all-reduce, clipping and the fused AdamW eager between
+    # replays).  Off by default: 79.4 ms graphed vs 78.7 ms eager per step
+    # (profiles/r6a) -- the gaps between the step's kernels are device-side
+    graphed = os.environ.get("VGGT_TRAIN_GRAPH", "0") == "1"
+    if graphed:
+        from aligned_vggt.runtime import GraphedStep
+        fwd_bwd = GraphedStep(fwd_bwd, modules=[head], warmup=2, device=dev)
+
+    def step():
+        fwd_bwd()
         if world > 1:  # one bucketed all-reduce of every gradient over RCCL (DDP semantics: mean)
             grads = [p.grad for p in head.parameters() if p.grad is not None]
             flat = torch.cat([g.reshape(-1) for g in grads])
@@ -459,7 +472,7 @@ def bench_train(args, world, rank, dev):
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (resident encoder tokens)",
             "config": {"workload": "train", "frames": S, "overlap": ov, "image": [H, W],
-                       "chunks_per_step": 2, "parallelism": "dp%d" % world}}), flush=True)
+                       "chunks_per_step": 2, "parallelism": "dp%d" % world, "hip_graph": graphed}}), flush=True)
 
 
 def bench_selftest(args, world, rank):

@@ -61,7 +61,7 @@ _CACHE = {}
 def _wt_bf16(lin: nn.Linear) -> torch.Tensor:
     """bf16 W^T [K, N] of a Linear (dX = dY W as vggt_gemm_bf16(dY, W^T)); cached per weight version."""
     w, _ = pack_linear(lin)
-    key = (w.data_ptr(), w._version)
+    key = lin.__dict__["_mi355x_pack"][0]  # the parameters' versions
     c = lin.__dict__.get("_mi355x_wt")
     if c is None or c[0] != key:
         c = (key, _transposed(w))
@@ -449,7 +449,7 @@ class TemporalBlockFn(torch.autograd.Function):
 def _kv_wt(attn) -> torch.Tensor:
     """bf16 [Wk; Wv]^T = [C, 2C]: dyn = [dk | dv] . [Wk; Wv] in one GEMM."""
     wkv, _ = attn.packed_kv()
-    key = (wkv.data_ptr(),)
+    key = attn.__dict__["_mi355x_kv"][0]
     c = attn.__dict__.get("_mi355x_kv_t")
     if c is None or c[0] != key:
         c = (key, _transposed(wkv))

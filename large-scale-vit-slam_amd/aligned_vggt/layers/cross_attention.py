@@ -22,7 +22,7 @@ import torch.nn as nn
 
 from .. import _native as N
 from ..backbone.layers import Attention, LayerScale, Mlp
-from ..runtime import Workspace, pack_linear
+from ..runtime import Workspace, _pkey, pack_linear
 from .. import autograd as AG
 
 
@@ -50,7 +50,7 @@ class CrossAttention(nn.Module):
         """bf16 [Wk; Wv] (2C x C) and rounded [bk; bv] -- one GEMM for k and v."""
         wk, bk = pack_linear(self.k)
         wv, bv = pack_linear(self.v)
-        key = (wk.data_ptr(), wv.data_ptr())
+        key = (self.k.__dict__["_mi355x_pack"][0], self.v.__dict__["_mi355x_pack"][0])  # parameter versions
         c = self.__dict__.get("_mi355x_kv")
         if c is None or c[0] != key:
             c = (key, torch.cat([wk, wv], 0).contiguous(), torch.cat([bk, bv], 0).contiguous())
@@ -58,7 +58,7 @@ class CrossAttention(nn.Module):
         return c[1], c[2]
 
     def f32_kv(self):
-        key = (self.k.weight.data_ptr(), self.k.weight._version, self.v.weight.data_ptr(), self.v.weight._version)
+        key = _pkey(self.k.weight, self.k.bias, self.v.weight, self.v.bias)
         c = self.__dict__.get("_mi355x_kv32")
         if c is None or c[0] != key:
             c = (key, torch.cat([self.k.weight, self.v.weight], 0).detach().float().contiguous(),

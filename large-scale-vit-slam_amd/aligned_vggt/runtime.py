@@ -92,3 +92,71 @@ class Workspace:
 
 def round_up(x: int, m: int) -> int:
     return (x + m - 1) // m * m
+
+
+# module-dict caches derived from parameter VALUES (bf16 packs, transposes,
+# concatenations); everything else cached on modules (RoPE tables, positions,
+# constant vectors) depends on shapes only
+WEIGHT_CACHES = ("_mi355x_pack", "_mi355x_wt", "_mi355x_kv")
+
+
+def drop_weight_caches(module: nn.Module) -> None:
+    """Forget every operand derived from a parameter's values, so the next
+    forward re-derives it (a HIP graph captured after this records the
+    re-derivation and repeats it on every replay, after each optimizer step)."""
+    for m in module.modules():
+        for k in [k for k in m.__dict__ if k.startswith(WEIGHT_CACHES)]:
+            del m.__dict__[k]
+
+
+class GraphedStep:
+    """One HIP graph for a launch-bound step.
+
+    The alignment-head training forward + backward is ~2,000 small kernels
+    per step (two chunks, 48 checkpoint-style block Functions, their HIP
+    backward kernels, the fused AdamW aside); issued eagerly through Python
+    and ctypes the device idles between many of them.  Captured once, the
+    whole sequence is replayed by one hipGraphLaunch.
+
+    ``fn`` must read only tensors whose storage stays put between calls
+    (parameters, resident inputs updated in place) and must not synchronise
+    with the host.  It runs ``warmup`` times eagerly on the capture stream
+    (settles workspace sizes and shape-keyed caches: RoPE tables, device
+    position vectors), then once under capture; the weight-derived caches of
+    ``modules`` are dropped first so the capture records their re-derivation
+    (parameters change in place between replays).  ``__call__`` replays and
+    returns the captured call's outputs (static tensors, overwritten by each
+    replay).  Gradients written by a captured backward are the static buffers
+    the capture allocated: do not ``zero_grad(set_to_none=True)`` between
+    replays (the captured step re-zeroes them itself)."""
+
+    def __init__(self, fn, modules=(), warmup: int = 2, device=None):
+        self.fn = fn
+        self.modules = list(modules)
+        self.warmup = warmup
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.graph = None
+        self.out = None
+
+    def capture(self) -> None:
+        if self.device.type != "cuda":
+            raise RuntimeError("GraphedStep: HIP graphs need a HIP device")
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(self.warmup):
+                self.fn()
+        s.synchronize()
+        for m in self.modules:
+            drop_weight_caches(m)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            self.out = self.fn()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self.graph = g
+
+    def __call__(self):
+        if self.graph is None:
+            self.capture()
+        self.graph.replay()
+        return self.out

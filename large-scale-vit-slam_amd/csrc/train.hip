@@ -78,6 +78,52 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__
   }
 }
 
+// Up to four finalizes of one reduction (same chunk count and length, e.g.
+// a LayerNorm's weight and bias sums) in one launch: blockIdx.y = vector.
+struct FinJobs {
+  const float* part[4];
+  int stride[4];
+  float* out[4];
+};
+
+__global__ __launch_bounds__(256) void finalize_multi_kernel(FinJobs jobs, int nchunk, int n, int accumulate) {
+  const int j = blockIdx.y;
+  __shared__ float red[16][17];
+  const float* __restrict__ part = jobs.part[j];
+  const int stride = jobs.stride[j];
+  const int col = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int i = blockIdx.x * 16 + col;
+  float s = 0.f;
+  if (i < n) {
+#pragma unroll 4
+    for (int c = sl; c < nchunk; c += 16) s += part[(int64_t)c * stride + i];
+  }
+  red[sl][col] = s;
+  __syncthreads();
+  if (sl == 0 && i < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][col];
+    float* out = jobs.out[j];
+    out[i] = accumulate ? out[i] + t : t;
+  }
+}
+
+// queue the non-null (part, stride, out) triples as one finalize_multi launch
+static void finalize_many(hipStream_t s, int nchunk, int n, int accumulate, int count, const float* const* parts,
+                          const int* strides, float* const* outs) {
+  FinJobs jobs{};
+  int k = 0;
+  for (int a = 0; a < count; ++a)
+    if (outs[a]) {
+      jobs.part[k] = parts[a];
+      jobs.stride[k] = strides[a];
+      jobs.out[k] = outs[a];
+      ++k;
+    }
+  if (k) finalize_multi_kernel<<<dim3((n + 15) / 16, k), 256, 0, s>>>(jobs, nchunk, n, accumulate);
+}
+
 // ------------------------------------------------------------ column sums
 // Block (x, y): columns [x*1024, x*1024+1024) in 4-column vectors, rows of
 // chunk y.  MODE 0: part0 = sum a                       (bias gradients)
@@ -882,8 +928,10 @@ extern "C" int vggt_layerscale_bwd(const float* dout, int64_t ldd, const void* b
   dim3 grid((N / 4 + 255) / 256, nc);
   colred_kernel<1><<<grid, 256, 0, s>>>(dout, VGGT_DTYPE_F32, ldd, branch, bdtype, ldb, gamma, dbranch, odtype, ldo,
                                         M, N, rpc, (float*)ws);
-  if (dgamma) finalize_kernel<<<(N + 15) / 16, 256, 0, s>>>((const float*)ws, nc, N, N, dgamma, 1);
-  if (dbias) finalize_kernel<<<(N + 15) / 16, 256, 0, s>>>((const float*)ws + (size_t)nc * N, nc, N, N, dbias, 1);
+  const float* parts[2] = {(const float*)ws, (const float*)ws + (size_t)nc * N};
+  const int strides[2] = {N, N};
+  float* outs[2] = {dgamma, dbias};
+  finalize_many(s, nc, N, 1, 2, parts, strides, outs);
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
 }
@@ -970,8 +1018,12 @@ extern "C" int vggt_layernorm_bwd(const void* x, int xdtype, int64_t ldx, const 
     case 4: launch_ln_bwd<4>(x, xdtype, ldx, w, eps, dy, dydtype, ldy, dx, dxdtype, lddx, accumulate, M, rm, nblk, rpb, part, s); break;
     default: return VGGT_ERR_SHAPE;
   }
-  if (dw) finalize_kernel<<<(C + 15) / 16, 256, 0, s>>>(part, nblk, C, C, dw, 1);
-  if (db) finalize_kernel<<<(C + 15) / 16, 256, 0, s>>>(part + (size_t)nblk * C, nblk, C, C, db, 1);
+  if (want) {
+    const float* parts[2] = {part, part + (size_t)nblk * C};
+    const int strides[2] = {C, C};
+    float* outs[2] = {dw, db};
+    finalize_many(s, nblk, C, 1, 2, parts, strides, outs);
+  }
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
 }
@@ -1017,8 +1069,9 @@ extern "C" int vggt_headnorm_rope_bwd(const void* pre, int64_t ldp, void* grad, 
   if (part) {
     float* outs[4] = {dw0, db0, dw1, db1};
     // part layout [blk][a][D] -> finalize each (a) slice with stride 4*D per block
-    for (int a = 0; a < 4; ++a)
-      if (outs[a]) finalize_kernel<<<(D + 15) / 16, 256, 0, s>>>(part + a * D, nblk, D, 4 * D, outs[a], 1);
+    const float* parts[4] = {part, part + D, part + 2 * D, part + 3 * D};
+    const int strides[4] = {4 * D, 4 * D, 4 * D, 4 * D};
+    finalize_many(s, nblk, D, 1, 4, parts, strides, outs);
   }
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
