@@ -135,6 +135,7 @@ TUNE_GEMM_TILE = 1
 TUNE_ATTN_WAVES = 2
 TUNE_ATTN_VARIANT = 3
 TUNE_CONV_PF2 = 4
+TUNE_ATTN16 = 5
 
 
 def tune(knob: int, value: int) -> int:

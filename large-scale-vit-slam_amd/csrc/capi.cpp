@@ -17,6 +17,7 @@ int env_or(const char* name, int dflt) {
 int g_vggt_gemm_tile = env_or("VGGT_GEMM", -1);
 int g_vggt_attn_waves = env_or("VGGT_ATTN_WAVES", 8);  // 8-wave groups for nq >= 4096 (profiles/r2c/ab_attn_w8)
 int g_vggt_attn_variant = env_or("VGGT_ATTN_VARIANT", 33);
+int g_vggt_attn16 = env_or("VGGT_ATTN16", 1);
 int g_vggt_conv_pf2 = env_or("VGGT_CONV_PF2", 1);
 
 extern "C" int vggt_tune(int knob, int value) {
@@ -37,12 +38,17 @@ extern "C" int vggt_tune(int knob, int value) {
       return prev;
     case VGGT_TUNE_ATTN_VARIANT:
       // 0-15: bit combinations of the max-tracking kernel; 19/23: pipelined QK^T;
-      // 32/33 (+64 exact scores): offset-free softmax
+      // 32/33 (+64 exact scores): offset-free softmax; 161 = 33 on the 16x16x32 MFMA shape (D = 64)
       if (value < 0 || (value > 15 && value != 19 && value != 23 && value != 32 && value != 33 && value != 96 &&
-                        value != 97))
+                        value != 97 && value != 161))
         return VGGT_ERR_UNSUPPORTED;
       prev = g_vggt_attn_variant;
       g_vggt_attn_variant = value;
+      return prev;
+    case VGGT_TUNE_ATTN16:
+      if (value != 0 && value != 1) return VGGT_ERR_UNSUPPORTED;
+      prev = g_vggt_attn16;
+      g_vggt_attn16 = value;
       return prev;
     case VGGT_TUNE_CONV_PF2:
       if (value != 0 && value != 1) return VGGT_ERR_UNSUPPORTED;

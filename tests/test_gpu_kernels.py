@@ -262,7 +262,7 @@ def _ref_attn(q, k, v, scale):
     return torch.softmax(s, -1) @ v.float()
 
 
-@pytest.mark.parametrize("variant", [3, 11, 15, 19, 23, 32, 97])
+@pytest.mark.parametrize("variant", [3, 11, 15, 19, 23, 32, 97, 161])
 @pytest.mark.parametrize("D,H,batch,n", [(64, 16, 3, 21), (64, 16, 2, 1374), (128, 8, 2, 1375), (64, 2, 1, 4100),
                                          (128, 2, 1, 64), (64, 1, 1, 1)])
 def test_attention_vs_torch(N, D, H, batch, n, variant):
@@ -321,7 +321,7 @@ def test_attention_global_shape_rows(N):
     assert _rel(o[rows], ref) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [3, 11, 19, 32, 96])
+@pytest.mark.parametrize("variant", [3, 11, 19, 32, 96, 161])
 def test_attention_online_softmax_rescale(N, variant):
     """Force the running max to jump late (rule 26): one key with a huge score
     in the last tile for some rows."""
@@ -332,7 +332,7 @@ def test_attention_online_softmax_rescale(N, variant):
         N.tune(N.TUNE_ATTN_VARIANT, prev)
 
 
-@pytest.mark.parametrize("variant", [32, 33, 96, 97])
+@pytest.mark.parametrize("variant", [32, 33, 96, 97, 161])
 @pytest.mark.parametrize("case", ["overflow_late", "all_negative", "huge_first_tile", "mixed_rows"])
 @pytest.mark.parametrize("waves,n", [(4, 700), (8, 4200)])
 def test_attention_offset_free_extremes(N, variant, case, waves, n):
@@ -487,3 +487,44 @@ def test_gemm_gelu_lut_exact(N, scale, tile):
         assert torch.equal(out.cpu().view(torch.int16), ref.view(torch.int16))
     finally:
         N.tune(N.TUNE_GEMM_TILE, prev)
+
+
+@pytest.mark.parametrize("batch,n,H", [(1, 21984, 2), (16, 1374, 4), (3, 51, 16), (3, 17, 16), (1, 6592, 2)])
+def test_attention16_accuracy_matches_32x32(N, batch, n, H):
+    """The 16x16x32 form (variant 161) against the 32x32x16 form (33) on the
+    same inputs, both against an fp64 host reference: the matrix-core shape
+    and the exact-restart softmax must not cost accuracy (rel-L2 within 10 %
+    of the 32x32 form's, and either form < 5e-3)."""
+    D = 64
+    C = H * D
+    g = torch.Generator().manual_seed(n + H)
+    qkv = (torch.randn(batch * n, 3 * C, generator=g) * 1.2).to(torch.bfloat16)
+    qkv_d = qkv.cuda()
+    outs = {}
+    for var in (33, 161):
+        prev = N.tune(N.TUNE_ATTN_VARIANT, var)
+        prev16 = N.tune(N.TUNE_ATTN16, 0)
+        try:
+            o = torch.empty(batch * n, C, device="cuda", dtype=torch.bfloat16)
+            N.attention(qkv_d[:, :C], qkv_d[:, C:2 * C], qkv_d[:, 2 * C:], o, batch, H, n, n, D, n, n, n)
+            outs[var] = o.double().cpu()
+        finally:
+            N.tune(N.TUNE_ATTN_VARIANT, prev)
+            N.tune(N.TUNE_ATTN16, prev16)
+    rows = torch.arange(batch * n) if batch * n <= 4096 else torch.randperm(batch * n, generator=g)[:2048]
+    t = qkv.double().view(batch, n, 3, H, D)
+    errs = {}
+    for var, o in outs.items():
+        num, den = 0.0, 0.0
+        for r in rows.tolist()[:2048]:
+            bi, qi = divmod(r, n)
+            q = t[bi, qi, 0]                      # (H, D)
+            k, v = t[bi, :, 1], t[bi, :, 2]       # (n, H, D)
+            s = torch.einsum("hd,nhd->hn", q, k) * D ** -0.5
+            ref = torch.einsum("hn,nhd->hd", torch.softmax(s, -1), v).reshape(C)
+            num += float(((o[r] - ref) ** 2).sum())
+            den += float((ref ** 2).sum())
+        errs[var] = (num / den) ** 0.5
+    print("rel-L2 vs fp64:", errs)
+    assert errs[161] < 5e-3 and errs[33] < 5e-3, errs
+    assert errs[161] <= 1.1 * errs[33] + 1e-5, errs
