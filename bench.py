@@ -276,7 +276,7 @@ def main():
             "mfma_util_whole_step": round(fl["total"] * value / world / (PEAK_BF16_TFLOPS * 1e12), 4),
             "mfma_util_pmc": _step_pmc(),
             "tflops_per_gpu": round(fl["total"] * value / world / 1e12, 1),
-            "roofline": {"bound": "mfma", "kernel": "attn16_fwd_kernel<8> (global attention, 1x16 heads x 21984^2 x 64)",
+            "roofline": {"bound": "mfma", "kernel": "attn_fwd_kernel<64> (global attention, 1x16 heads x 21984^2 x 64)",
                          "achieved": round(attn_tflops, 1) if attn_tflops else None, "peak": PEAK_BF16_TFLOPS,
                          "unit": "TFLOP/s",
                          "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4) if attn_tflops else None,

@@ -820,9 +820,11 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
   const int nw = (g_vggt_attn_waves == 8 && nq >= 4096) ? 8 : (g_vggt_attn_waves == 2 && two_ok) ? 2 : 4;
   const int nwg = ((nq + nw * 32 - 1) / (nw * 32)) * heads * batch;
   hipStream_t s = (hipStream_t)stream;
-  // 16x16x32 matrix-core form: variant 161 forces it; the default 33 takes it
-  // for D = 64 unless VGGT_ATTN16=0 (profiles/r6c: global 16 x 21,984^2 x 64
-  // 1.80 vs 1.83 ms, frame 16 x 16 x 1374^2 x 64 128-134 vs 135-137 us)
+  // 16x16x32 matrix-core form: variant 161 forces it; variant 33 takes it for
+  // D = 64 when VGGT_ATTN16=1.  Off by default: faster back to back in kbench
+  // (profiles/r6c: global 1.80 vs 1.83 ms, frame 128-134 vs 135-137 us) but not
+  // in the model (r6d: global 1.87 vs 1.84 ms per launch, step 100.8 vs 100.5
+  // ms, configs[3] 1329 vs 1299 ms)
   const bool use16 = D == 64 && nw != 2 && (g_vggt_attn_variant == 161 || (g_vggt_attn_variant == 33 && g_vggt_attn16));
   if (use16) {
     if (nw == 8) attn16_fwd_kernel<8><<<nwg, 512, 0, s>>>(a);

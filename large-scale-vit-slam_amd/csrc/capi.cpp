@@ -17,7 +17,7 @@ int env_or(const char* name, int dflt) {
 int g_vggt_gemm_tile = env_or("VGGT_GEMM", -1);
 int g_vggt_attn_waves = env_or("VGGT_ATTN_WAVES", 8);  // 8-wave groups for nq >= 4096 (profiles/r2c/ab_attn_w8)
 int g_vggt_attn_variant = env_or("VGGT_ATTN_VARIANT", 33);
-int g_vggt_attn16 = env_or("VGGT_ATTN16", 1);
+int g_vggt_attn16 = env_or("VGGT_ATTN16", 0);  // measured slower in the model (profiles/r6d)
 int g_vggt_conv_pf2 = env_or("VGGT_CONV_PF2", 1);
 
 extern "C" int vggt_tune(int knob, int value) {

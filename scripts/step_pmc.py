@@ -37,7 +37,7 @@ def get(r, *names):
 
 
 def classify(name):
-    if "attn_fwd" in name:
+    if "attn_fwd" in name or "attn16_fwd" in name:
         return "attention"
     if "gemm" in name:
         return "gemm"
