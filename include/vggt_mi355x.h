@@ -452,9 +452,12 @@ int vggt_attention_small_bwd(const void* q, int64_t ldq, int64_t q_bstride, cons
  * alignment head): x = the forward input, dy the output gradient, same row
  * map as vggt_layernorm_grouped (logical row r -> group r/group; x and dx rows
  * g*x_group_stride + x_row_offset + i, dy rows g*y_group_stride +
- * y_row_offset + i).  dx (+)= (accumulate: f32 only).  dw/db (may be NULL)
- * get the parameter gradients added.  C % 256 == 0, C <= 1024.
+ * y_row_offset + i).  accumulate: bit VGGT_LN_BWD_DX_ACCUMULATE (1) dx += (f32
+ * only, else dx =); dw/db (may be NULL) get the parameter gradients added, or
+ * written with bit VGGT_LN_BWD_PARAMS_WRITE (2).  C % 256 == 0, C <= 1024.
  */
+#define VGGT_LN_BWD_DX_ACCUMULATE 1
+#define VGGT_LN_BWD_PARAMS_WRITE 2
 size_t vggt_layernorm_bwd_workspace_bytes(int M, int C);
 int vggt_layernorm_bwd(const void* x, int xdtype, int64_t ldx, const float* w, float eps, const void* dy, int dydtype,
                        int64_t ldy, void* dx, int dxdtype, int64_t lddx, int accumulate, int M, int C, int group,
@@ -524,6 +527,9 @@ int vggt_wgrad_bf16(const void* dy, int64_t ldy, const void* x, int64_t ldx, int
 /* dW[n, k] (+)= sum_m dY[m, n] X[m, k]  fp32 (skinny-M decoder / gated-update Linear weight gradients). */
 int vggt_wgrad_f32(const float* dy, int64_t ldy, const float* x, int64_t ldx, int M, int N, int K, float* dw,
                    int64_t ldw, int accumulate, void* stream);
+/* The same and db[n] (+)= sum_m dY[m, n] in the one launch (LinearF32Fn backward: weight and bias gradients). */
+int vggt_wgrad_bias_f32(const float* dy, int64_t ldy, const float* x, int64_t ldx, int M, int N, int K, float* dw,
+                        int64_t ldw, float* db, int accumulate, void* stream);
 
 /* out[b] = sum_{i<n} a[b*bs + i] * c[b*bs + i]  (d chunk_scale of depth *= chunk_scale,
  * featureAligned_vggt.py:171, in training).  ws >= vggt_batch_dot_workspace_bytes(B, n). */

@@ -89,6 +89,7 @@ _SIGS = {
     "vggt_headnorm_rope_out": [_vp, _i64, _vp, _i64, _i, _i, _i, _vp, _vp, _f, _i, _vp, _i, _vp, _vp, _i, _vp],
     "vggt_transpose_b16": [_vp, _i64, _i, _i, _vp, _i64, _i, _vp],
     "vggt_wgrad_f32": [_vp, _i64, _vp, _i64, _i, _i, _i, _vp, _i64, _i, _vp],
+    "vggt_wgrad_bias_f32": [_vp, _i64, _vp, _i64, _i, _i, _i, _vp, _i64, _vp, _i, _vp],
     "vggt_wgrad_bf16": [_vp, _i64, _vp, _i64, _i, _i, _i, _vp, _i64, _i, _vp, ctypes.c_size_t, _vp],
     "vggt_batch_dot_f32": [_vp, _vp, _i64, _i, _i64, _vp, _vp, ctypes.c_size_t, _vp],
 }
@@ -656,9 +657,10 @@ def attention_small_bwd(q, k, v, do, dq, dk, dv, batch: int, heads: int, nq: int
 
 def layernorm_bwd(x, w, eps: float, dy, dx, accumulate: bool, dw=None, db=None, M: Optional[int] = None,
                   group: Optional[int] = None, x_gstride: int = 0, x_off: int = 0, y_gstride: int = 0,
-                  y_off: int = 0) -> None:
-    """dx (+)= LayerNorm backward; dw/db (+)= parameter gradients.  Identity
-    row map unless group/strides are given (vggt_layernorm_grouped's)."""
+                  y_off: int = 0, params_write: bool = False) -> None:
+    """dx (+)= LayerNorm backward; dw/db (+)= parameter gradients (written
+    instead with params_write).  Identity row map unless group/strides are
+    given (vggt_layernorm_grouped's)."""
     _dev(x, "layernorm_bwd")
     M = x.shape[0] if M is None else M
     C = x.shape[1]
@@ -667,7 +669,8 @@ def layernorm_bwd(x, w, eps: float, dy, dx, accumulate: bool, dw=None, db=None, 
     ws = _train_ws(x.device, nb)
     g = (M if M > 0 else 1) if group is None else group
     rc = L.vggt_layernorm_bwd(_p(x), _dt(x), _ld(x), _p(w), float(eps), _p(dy), _dt(dy), _ld(dy), _p(dx), _dt(dx),
-                              _ld(dx), int(accumulate), M, C, g, x_gstride, x_off, y_gstride, y_off, _p(dw), _p(db),
+                              _ld(dx), int(accumulate) | (2 if params_write else 0), M, C, g, x_gstride, x_off, y_gstride,
+                              y_off, _p(dw), _p(db),
                               _p(ws), ws.numel() * 4, _stream())
     _check(rc, "vggt_layernorm_bwd")
 
@@ -769,6 +772,17 @@ def wgrad_f32(dy, x, dw, accumulate: bool = True) -> None:
     assert x.shape[0] == M and dw.shape == (N_, K)
     rc = lib().vggt_wgrad_f32(_p(dy), _ld(dy), _p(x), _ld(x), M, N_, K, _p(dw), _ld(dw), int(accumulate), _stream())
     _check(rc, "vggt_wgrad_f32")
+
+
+def wgrad_bias_f32(dy, x, dw, db, accumulate: bool = False) -> None:
+    """dw (+)= dy^T x and db (+)= column sums of dy in one launch (fp32)."""
+    _dev(dy, "wgrad_bias_f32")
+    M, N_ = dy.shape
+    K = x.shape[1]
+    assert x.shape[0] == M and dw.shape == (N_, K) and db.shape == (N_,) and db.is_contiguous()
+    rc = lib().vggt_wgrad_bias_f32(_p(dy), _ld(dy), _p(x), _ld(x), M, N_, K, _p(dw), _ld(dw), _p(db),
+                                   int(accumulate), _stream())
+    _check(rc, "vggt_wgrad_bias_f32")
 
 
 def batch_dot_f32(a, c, out) -> None:

@@ -563,15 +563,13 @@ class LinearF32Fn(torch.autograd.Function):
                 dpre.copy_(dy2 * (cdf + xx * torch.exp(-0.5 * xx * xx) * 0.3989422804014327))
         else:
             dpre = dy2
+        dw = torch.empty_like(w, dtype=torch.float32)  # written (not accumulated): every element
         db = None
-        if ctx.has_b:
-            if Nn % 4 == 0:
-                db = torch.empty(Nn, device=dy.device)  # written, not accumulated
-                N.colsum(dpre, db, False)
-            else:
-                db = dpre.sum(0)
-        dw = torch.empty_like(w, dtype=torch.float32)  # vggt_wgrad_f32 without accumulate writes every element
-        N.wgrad_f32(dpre, x2, dw, False)
+        if ctx.has_b:  # weight and bias gradients in one launch
+            db = torch.empty(Nn, device=dy.device)
+            N.wgrad_bias_f32(dpre, x2, dw, db, False)
+        else:
+            N.wgrad_f32(dpre, x2, dw, False)
         dx = None
         if ctx.needs_input_grad[0]:
             wt = _wt_f32(w, ctx.owner, ctx.name)
@@ -600,9 +598,8 @@ class LayerNormF32Fn(torch.autograd.Function):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(x2.shape).float().contiguous()
         dx = torch.empty_like(x2)
-        ar = _GradArena(dx.device, [w, w])  # the parameter sums accumulate into zeroed outputs
-        dw, db = ar.like(w), ar.like(w)
-        N.layernorm_bwd(x2, w.detach(), ctx.eps, dy2, dx, False, dw, db)
+        dw, db = torch.empty_like(x2[0]), torch.empty_like(x2[0])  # written by the finalize (no zero fill)
+        N.layernorm_bwd(x2, w.detach(), ctx.eps, dy2, dx, False, dw, db, params_write=True)
         return dx.view(ctx.shape), dw, db, None
 
 

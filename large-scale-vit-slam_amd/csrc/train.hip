@@ -637,15 +637,21 @@ __global__ __launch_bounds__(256) void attn_small_bwd_kernel(
 // dW[n][k] (+)= sum_m dY[m][n] * X[m][k]  (skinny M: the fp32 decoder /
 // gated-update linears, M = batch * frames <= a few hundred).  Thread per
 // output, 64 consecutive k per wave (coalesced X reads), dY[m][n] broadcast.
+// db != NULL: column k == K is the bias (an all-ones X column), db[n] = sum_m dY[m, n]
 __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict__ dy, int64_t ldy,
                                                         const float* __restrict__ x, int64_t ldx, int M, int N, int K,
-                                                        float* __restrict__ dw, int64_t ldw, int accumulate) {
+                                                        float* __restrict__ dw, int64_t ldw, int accumulate,
+                                                        float* __restrict__ db) {
   const int k = blockIdx.x * 256 + threadIdx.x;
   const int n = blockIdx.y;
-  if (k >= K) return;
+  if (k > K || (k == K && !db)) return;
   float s = 0.f;
-  for (int m = 0; m < M; ++m) s += dy[(int64_t)m * ldy + n] * x[(int64_t)m * ldx + k];
-  float* o = dw + (int64_t)n * ldw + k;
+  if (k < K) {
+    for (int m = 0; m < M; ++m) s += dy[(int64_t)m * ldy + n] * x[(int64_t)m * ldx + k];
+  } else {
+    for (int m = 0; m < M; ++m) s += dy[(int64_t)m * ldy + n];
+  }
+  float* o = k < K ? dw + (int64_t)n * ldw + k : db + n;
   *o = accumulate ? *o + s : s;
 }
 
@@ -1003,6 +1009,9 @@ extern "C" int vggt_layernorm_bwd(const void* x, int xdtype, int64_t ldx, const 
                                   int y_row_offset, float* dw, float* db, void* ws, size_t ws_bytes, void* stream) {
   if (M <= 0) return M == 0 ? VGGT_OK : VGGT_ERR_SHAPE;
   if (C % 256 || C > 1024 || group <= 0) return VGGT_ERR_SHAPE;
+  if (accumulate & ~(VGGT_LN_BWD_DX_ACCUMULATE | VGGT_LN_BWD_PARAMS_WRITE)) return VGGT_ERR_UNSUPPORTED;
+  const int param_acc = (accumulate & VGGT_LN_BWD_PARAMS_WRITE) ? 0 : 1;
+  accumulate &= VGGT_LN_BWD_DX_ACCUMULATE;
   if (accumulate && dxdtype != VGGT_DTYPE_F32) return VGGT_ERR_UNSUPPORTED;
   if ((ldx | ldy | lddx) % 4 || ((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx) % 8) return VGGT_ERR_ALIGN;
   const int nblk = nchunks_for(M, ROWBWD_MAXC, ROWBWD_ROWS);
@@ -1022,7 +1031,7 @@ extern "C" int vggt_layernorm_bwd(const void* x, int xdtype, int64_t ldx, const 
     const float* parts[2] = {part, part + (size_t)nblk * C};
     const int strides[2] = {C, C};
     float* outs[2] = {dw, db};
-    finalize_many(s, nblk, C, 1, 2, parts, strides, outs);
+    finalize_many(s, nblk, C, param_acc, 2, parts, strides, outs);
   }
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
@@ -1107,7 +1116,17 @@ extern "C" int vggt_wgrad_f32(const float* dy, int64_t ldy, const float* x, int6
   if (M <= 0 || N <= 0 || K <= 0) return VGGT_ERR_SHAPE;
   if (N > 65535) return VGGT_ERR_SHAPE;
   dim3 grid((K + 255) / 256, N);
-  wgrad_f32_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(dy, ldy, x, ldx, M, N, K, dw, ldw, accumulate);
+  wgrad_f32_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(dy, ldy, x, ldx, M, N, K, dw, ldw, accumulate, nullptr);
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+extern "C" int vggt_wgrad_bias_f32(const float* dy, int64_t ldy, const float* x, int64_t ldx, int M, int N, int K,
+                                   float* dw, int64_t ldw, float* db, int accumulate, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || !db) return VGGT_ERR_SHAPE;
+  if (N > 65535) return VGGT_ERR_SHAPE;
+  dim3 grid((K + 1 + 255) / 256, N);
+  wgrad_f32_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(dy, ldy, x, ldx, M, N, K, dw, ldw, accumulate, db);
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
 }

@@ -115,6 +115,11 @@ def test_layernorm_bwd(N, C, xdt, dydt, acc):
     F.layer_norm(xr, (C,), wr, br, 1e-5).backward(dy.float())
     ref = xr.grad + (dx0 if acc else 0)
     assert _rel(dx, ref) < 1e-5 and _rel(dw, wr.grad) < 1e-5 and _rel(db, br.grad) < 1e-5
+    # params_write: dw / db written, not added (no zero fill needed)
+    dw2, db2 = torch.full((C,), 9.0, device="cuda"), torch.full((C,), 9.0, device="cuda")
+    dx2 = dx0.clone() if acc else torch.empty(M, C, device="cuda", dtype=torch.float32)
+    N.layernorm_bwd(x, w, 1e-5, dy, dx2, acc, dw2, db2, params_write=True)
+    assert torch.equal(dw2, dw) and torch.equal(db2, db) and torch.equal(dx2, dx)
 
 
 def test_layernorm_bwd_grouped(N):
@@ -233,6 +238,14 @@ def test_transpose_wgrad_batchdot(N):
     dw = torch.zeros(300, 1536, device="cuda")
     N.wgrad_f32(dy, x, dw, True)
     assert _rel(dw, dy.t() @ x) < 1e-5
+    # weight + bias gradient in one launch (K = 256 puts the bias column in a block of its own)
+    for K in (1536, 256, 7):
+        x = torch.randn(9, K, device="cuda")
+        dw, db = torch.full((300, K), 5.0, device="cuda"), torch.full((300,), 5.0, device="cuda")
+        N.wgrad_bias_f32(dy, x, dw, db, False)
+        assert _rel(dw, dy.t() @ x) < 1e-5 and _rel(db, dy.sum(0)) < 1e-5
+        N.wgrad_bias_f32(dy, x, dw, db, True)
+        assert _rel(dw, 2 * dy.t() @ x) < 1e-5 and _rel(db, 2 * dy.sum(0)) < 1e-5
     a, c = torch.randn(3, 2, 50, 60, device="cuda"), torch.randn(3, 2, 50, 60, device="cuda")
     out = torch.empty(3, device="cuda")
     N.batch_dot_f32(a, c, out)
