@@ -33,6 +33,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "large-scale-vit-slam_amd"))
 sys.path.insert(0, ROOT)
 
+# kernel arguments in device memory (see aligned_vggt/__init__.py), set before
+# the HIP runtime initialises
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 import torch  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
