@@ -60,7 +60,11 @@ const char* vggt_version(void);
 #define VGGT_TUNE_ATTN_WAVES 2 /* 2, 4 or 8 waves (64 / 128 / 256 query rows) per attention workgroup */
 #define VGGT_TUNE_ATTN_VARIANT 3 /* 0-15: attention instruction-schedule variant bits */
 #define VGGT_TUNE_CONV_PF2 4     /* split-bf16 conv gather: 1 two-deep (buffer loads, default), 0 one-deep */
-#define VGGT_TUNE_ATTN16 5       /* 1: D = 64 attention on the 16x16x32 matrix-core form, 0: 32x32x16 (default) */
+#define VGGT_TUNE_ATTN16 5       /* 1: D = 64 attention on the 16x16x32 matrix-core form, 0: 32x32x16 (default),
+                                    2: 16x16x32 for 4-wave (nq < 4096) launches only */
+#define VGGT_TUNE_GEMM_PIPE 6    /* persistent GEMM K-loop DMA placement bits (gemm.hip): 1 half 0 waits for its
+                                    K-tile at the end of MATH, 2 half 1 stages K-tile kt+2 inside MATH(kt),
+                                    4 half 0 issues every W piece, no READ waits on DMA */
 int vggt_tune(int knob, int value);
 
 /*

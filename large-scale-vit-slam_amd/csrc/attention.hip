@@ -825,7 +825,10 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
   // (profiles/r6c: global 1.80 vs 1.83 ms, frame 128-134 vs 135-137 us) but not
   // in the model (r6d: global 1.87 vs 1.84 ms per launch, step 100.8 vs 100.5
   // ms, configs[3] 1329 vs 1299 ms)
-  const bool use16 = D == 64 && nw != 2 && (g_vggt_attn_variant == 161 || (g_vggt_attn_variant == 33 && g_vggt_attn16));
+  // VGGT_ATTN16=2: the 16x16 form only for the 4-wave (nq < 4096: frame / DINOv2) launches
+  const bool use16 = D == 64 && nw != 2 &&
+                     (g_vggt_attn_variant == 161 ||
+                      (g_vggt_attn_variant == 33 && (g_vggt_attn16 == 1 || (g_vggt_attn16 == 2 && nw == 4))));
   if (use16) {
     if (nw == 8) attn16_fwd_kernel<8><<<nwg, 512, 0, s>>>(a);
     else attn16_fwd_kernel<4><<<nwg, 256, 0, s>>>(a);

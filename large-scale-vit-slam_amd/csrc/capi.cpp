@@ -19,6 +19,7 @@ int g_vggt_attn_waves = env_or("VGGT_ATTN_WAVES", 8);  // 8-wave groups for nq >
 int g_vggt_attn_variant = env_or("VGGT_ATTN_VARIANT", 33);
 int g_vggt_attn16 = env_or("VGGT_ATTN16", 0);  // measured slower in the model (profiles/r6d)
 int g_vggt_conv_pf2 = env_or("VGGT_CONV_PF2", 1);
+int g_vggt_gemm_pipe = env_or("VGGT_GEMM_PIPE", 0);
 
 extern "C" int vggt_tune(int knob, int value) {
   int prev;
@@ -46,7 +47,7 @@ extern "C" int vggt_tune(int knob, int value) {
       g_vggt_attn_variant = value;
       return prev;
     case VGGT_TUNE_ATTN16:
-      if (value != 0 && value != 1) return VGGT_ERR_UNSUPPORTED;
+      if (value < 0 || value > 2) return VGGT_ERR_UNSUPPORTED;
       prev = g_vggt_attn16;
       g_vggt_attn16 = value;
       return prev;
@@ -54,6 +55,11 @@ extern "C" int vggt_tune(int knob, int value) {
       if (value != 0 && value != 1) return VGGT_ERR_UNSUPPORTED;
       prev = g_vggt_conv_pf2;
       g_vggt_conv_pf2 = value;
+      return prev;
+    case VGGT_TUNE_GEMM_PIPE:
+      if (value < 0 || value > 7) return VGGT_ERR_UNSUPPORTED;
+      prev = g_vggt_gemm_pipe;
+      g_vggt_gemm_pipe = value;
       return prev;
     default: return VGGT_ERR_UNSUPPORTED;
   }

@@ -1159,6 +1159,13 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
 #pragma unroll
     for (int i = 0; i < C::WL; ++i) dma16s(rw, woff[i], soff, b + C::ABYTES + (wave * C::WL + i) * 1024);
   };
+  // the W pieces of the other wave half (rows + 128: the swizzle is row & 7, the same)
+  auto stage_w2 = [&](int buf, int kt) {
+    const uint32_t b = lds0 + buf * C::BUF;
+    const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(kt * PBK * 2 + 4 * C::WL * 8 * ldw * 2));
+#pragma unroll
+    for (int i = 0; i < C::WL; ++i) dma16s(rw, woff[i], soff, b + C::ABYTES + ((wave + 4) * C::WL + i) * 1024);
+  };
   auto stage_a = [&](int buf, int kt) {
     const uint32_t b = lds0 + buf * C::BUF;
     const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(kt * PBK * 2));
@@ -1208,6 +1215,33 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
     __builtin_amdgcn_s_setprio(0);
   };
 
+  // math2 with (when `st`) K-tile skt's DMA pieces (W, then A) spread over the MFMA
+  // stream: piece p after MFMA (p + 1) * TOT / (LPS + 1) - 1, behind a wave-uniform
+  // branch so the register allocation is math2's
+  auto math2_stage = [&](bool st, int sbuf, int skt) {
+    if constexpr (!FK) return;
+    constexpr int TOT = 2 * C::MI * C::NI;
+    const uint32_t b = lds0 + sbuf * C::BUF;
+    const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(skt * PBK * 2));
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < TOT; ++i) {
+      const int h = i / (C::MI * C::NI), r = i % (C::MI * C::NI), mi = r / C::NI, ni = r % C::NI;
+      acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h ? wf2[ni] : wf[ni], h ? af2[mi] : af[mi], acc[ni][mi], 0, 0, 0);
+#pragma unroll
+      for (int p = 0; p < LPS; ++p)
+        if (i == (p + 1) * TOT / (LPS + 1) - 1) {
+          __builtin_amdgcn_sched_barrier(0);
+          if (st) {
+            if (p < C::WL) dma16s(rw, woff[p], soff, b + C::ABYTES + (wave * C::WL + p) * 1024);
+            else dma16s(ra, aoff[p - C::WL], soff, b + (wave * C::AL + p - C::WL) * 1024);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
   int tile = blockIdx.x;
   if (tile >= ntiles) return;
   // prologue: the first tile's K-tiles 0 and 1
@@ -1231,6 +1265,19 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
       for (int j = 0; j < C::MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (wm == 1) asm volatile("s_barrier" ::: "memory");  // stagger the second M half by one segment
     if constexpr (FK) {
+      // DMA placement (sched bits 9-10, VGGT_TUNE_GEMM_PIPE): with bit 9 half 0 no longer waits for the
+      // K-tile kt+1 pieces it issued at READ(kt) before READ(kt)'s barrier but at the end of MATH(kt)
+      // (half 0 reads them first, at READ(kt+1)); with bit 10 half 1 issues no DMA in its READ
+      // segments and instead stages K-tile kt+2 inside MATH(kt), one piece per MFMA group (the buffer
+      // of K-tile kt is free by then: both halves read it in the two segments before), waiting for
+      // them at the end of its next READ.  Either way every wait covers pieces issued at least one
+      // segment earlier, so no READ segment carries a DMA round trip.
+      // Bit 11 (with bit 9): half 0 issues every W piece of K-tile kt+1 (its own and half 1's rows,
+      // the latter 128 rows on through the scalar offset) and half 1 only its A pieces, which it then
+      // waits for at the end of MATH(kt) like half 0 -- no READ segment waits on DMA at all.
+      const bool wall = (sched >> 11) & 1;
+      const bool dh0 = (((sched >> 9) & 1) && wm == 0) || wall;
+      const bool mh1 = ((sched >> 10) & 1) && wm == 1 && !wall;
       for (int kt = 0; kt < nk; ++kt) {
         const int buf = (b0 + kt) & 1;
         const bool pf = kt >= 1 && kt + 1 < nk;
@@ -1238,19 +1285,29 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
         // The W pieces (read by both wave halves from the next segment on) land
         // before this segment's barrier, the A pieces (read by this half two
         // segments later) before the MATH segment's.
-        if (pf) {
+        if (pf && wall) {
+          if (wm == 0) {
+            stage_w(buf ^ 1, kt + 1);
+            stage_w2(buf ^ 1, kt + 1);
+          }
+          stage_a(buf ^ 1, kt + 1);
+        } else if (pf && !mh1) {
           stage_w(buf ^ 1, kt + 1);
           stage_a(buf ^ 1, kt + 1);
         }
         read_frags(buf, 0);
         read_frags2(buf);
-        if (pf) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::AL) : "memory");
+        if (dh0 && !(wall && wm == 1 && kt == 0)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else if (pf && !mh1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::AL) : "memory");
         else if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NST) : "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
-        math2();
+        math2_stage(mh1 && kt + 2 < nk, buf, kt + 2);
         __builtin_amdgcn_sched_barrier(0);
-        if (pf) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        if (dh0 && !(wall && wm == 1 && kt == 0)) {
+          if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NST) : "memory");
+          else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        } else if (pf && !mh1) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
         else asm volatile("s_barrier" ::: "memory");
       }
     } else
@@ -1548,7 +1605,7 @@ int launch_ppp_fk(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, in
     const char* d = getenv("VGGT_GEMM_SPLITDMA");
     return (e ? atoi(e) & 255 : 4) | (d && !atoi(d) ? 0 : 256);
   }();
-  gemm_ppp_kernel<EPI, BMT, FK><<<nwg, PNT, lds, s>>>(a, lda, w, ldw, M, N, K, ep, sched);
+  gemm_ppp_kernel<EPI, BMT, FK><<<nwg, PNT, lds, s>>>(a, lda, w, ldw, M, N, K, ep, sched | (g_vggt_gemm_pipe & 7) << 9);
   return VGGT_OK;
 }
 

@@ -3,5 +3,6 @@
 extern int g_vggt_gemm_tile;   // -1 auto, 0 128x128, 1 256x256 ring, 2 256x128 ring, 3-7 ping-pong, 8 two-per-CU, 9 persistent ping-pong
 extern int g_vggt_attn_waves;  // 2, 4 or 8 (8: only for nq >= 4096; 2: offset-free variant 33 only)
 extern int g_vggt_attn_variant; // attention schedule variant bits (attention.hip)
-extern int g_vggt_attn16;       // 1: variant 33 runs the 16x16x32 form for D = 64 (attn16_fwd_kernel); default 0
+extern int g_vggt_attn16;       // 1: variant 33 runs the 16x16x32 form for D = 64 (attn16_fwd_kernel), 2: only for 4-wave launches; default 0
 extern int g_vggt_conv_pf2;     // split-bf16 conv: 1 two-deep buffer-load gather, 0 one-deep
+extern int g_vggt_gemm_pipe;    // persistent GEMM DMA placement bits (VGGT_TUNE_GEMM_PIPE)
