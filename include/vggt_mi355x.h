@@ -64,7 +64,9 @@ const char* vggt_version(void);
                                     2: 16x16x32 for 4-wave (nq < 4096) launches only */
 #define VGGT_TUNE_GEMM_PIPE 6    /* persistent GEMM K-loop DMA placement bits (gemm.hip): 1 half 0 waits for its
                                     K-tile at the end of MATH, 2 half 1 stages K-tile kt+2 inside MATH(kt),
-                                    4 half 0 issues every W piece, no READ waits on DMA */
+                                    4 half 0 issues every W piece, no READ waits on DMA,
+                                    8 half 0's epilogue overlaps half 1's last MATH segment, 16 bit 4 in the
+                                    half-K loop; default 5 */
 int vggt_tune(int knob, int value);
 
 /*

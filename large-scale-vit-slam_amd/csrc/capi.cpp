@@ -17,9 +17,13 @@ int env_or(const char* name, int dflt) {
 int g_vggt_gemm_tile = env_or("VGGT_GEMM", -1);
 int g_vggt_attn_waves = env_or("VGGT_ATTN_WAVES", 8);  // 8-wave groups for nq >= 4096 (profiles/r2c/ab_attn_w8)
 int g_vggt_attn_variant = env_or("VGGT_ATTN_VARIANT", 33);
-int g_vggt_attn16 = env_or("VGGT_ATTN16", 0);  // measured slower in the model (profiles/r6d)
+// 2: the 16x16x32 form for the 4-wave (frame / DINOv2) launches only -- all launches measured slower in the model
+// (profiles/r6d), frame-only faster (r7b: step 98.9-99.0 -> 98.3 ms)
+int g_vggt_attn16 = env_or("VGGT_ATTN16", 2);
 int g_vggt_conv_pf2 = env_or("VGGT_CONV_PF2", 1);
-int g_vggt_gemm_pipe = env_or("VGGT_GEMM_PIPE", 0);
+// 5: half 0 issues every W piece and no READ segment waits on DMA in the whole-K-tile loop
+// (profiles/r7c/r7d: aggregator step 102.4 -> 99.3 ms with the frame-only 16x16 attention, same box)
+int g_vggt_gemm_pipe = env_or("VGGT_GEMM_PIPE", 5);
 
 extern "C" int vggt_tune(int knob, int value) {
   int prev;
@@ -57,7 +61,7 @@ extern "C" int vggt_tune(int knob, int value) {
       g_vggt_conv_pf2 = value;
       return prev;
     case VGGT_TUNE_GEMM_PIPE:
-      if (value < 0 || value > 7) return VGGT_ERR_UNSUPPORTED;
+      if (value < 0 || value > 31) return VGGT_ERR_UNSUPPORTED;
       prev = g_vggt_gemm_pipe;
       g_vggt_gemm_pipe = value;
       return prev;

@@ -75,6 +75,20 @@ __device__ __forceinline__ uint32_t gelu2_lut(uint32_t d, TP lut) {
   }
   return gelu1_lut(d & 0xffff, lut) | (gelu1_lut(d >> 16, lut) << 16);
 }
+// Branch-free form for a group of packed pairs: both halves' indices clamped into the
+// table (packed u16 ops), so every lookup is issued with no control flow in between;
+// `oor` collects whether any half was clamped, and the caller re-does the group with
+// gelu2_lut (a wave-uniform branch per group, rare) when a lane saw one.
+__device__ __forceinline__ uint32_t gelu2_clamped(uint32_t d, const uint16_t* lut, uint32_t& oor) {
+  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+  const us2 m = __builtin_bit_cast(us2, d & 0x7fff7fffu);
+  const us2 t = m - (us2)(unsigned short)(GELU_LUT_E0 << 7);                // wraps below the table
+  const us2 tc = __builtin_elementwise_min(t, (us2)(unsigned short)(GELU_LUT_N - 1));
+  oor |= __builtin_bit_cast(uint32_t, t) ^ __builtin_bit_cast(uint32_t, tc);
+  const us2 sg = __builtin_bit_cast(us2, (d >> 15) & 0x00010001u);
+  const uint32_t ix = __builtin_bit_cast(uint32_t, (us2)(tc + sg * (us2)(unsigned short)GELU_LUT_N));
+  return (uint32_t)lut[ix & 0xffff] | ((uint32_t)lut[ix >> 16] << 16);
+}
 // the global-memory table (the LDS-staged epilogues of the one-shot forms)
 __device__ __forceinline__ uint32_t gelu2_tab(uint32_t d, const uint16_t* lut) { return gelu2_lut(d, lut); }
 
@@ -1310,13 +1324,22 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
         } else if (pf && !mh1) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
         else asm volatile("s_barrier" ::: "memory");
       }
-    } else
+    } else {
+    // (sched bit 13; measured slower for the fused qkv GEMM: 147.3-148.6 -> 150.4-151.2 us, r7d)
+    const bool wall_h = (sched >> 13) & 1;
     for (int kt = 0; kt < nk; ++kt) {
       const int buf = (b0 + kt) & 1;
       const bool pf = kt >= 1 && kt + 1 < nk;  // this step issues K-tile kt+1 (K-tile 1 was issued ahead)
       // READ(kt, 0): K-tile kt+1's DMA (split: its W half), this step's fragments
       if (pf) {
-        if (split) stage_w(buf ^ 1, kt + 1);
+        if (split && wall_h) {
+          // (sched bit 13) half 0 issues every W piece of K-tile kt+1 and waits for
+          // them at the end of MATH(kt, 1), three segments on; half 1 issues none
+          if (wm == 0) {
+            stage_w(buf ^ 1, kt + 1);
+            stage_w2(buf ^ 1, kt + 1);
+          }
+        } else if (split) stage_w(buf ^ 1, kt + 1);
         else stage(buf ^ 1, kt + 1);
       }
       read_frags(buf, 0);
@@ -1331,7 +1354,8 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
       if (pf && split) {
         stage_a(buf ^ 1, kt + 1);
         read_frags(buf, 1);
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::AL) : "memory");
+        if (wall_h) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::AL) : "memory");
       } else {
         read_frags(buf, 1);
         if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NST) : "memory");
@@ -1343,8 +1367,17 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
       if (pf && split) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
       else asm volatile("s_barrier" ::: "memory");
     }
-    if (wm == 0) asm volatile("s_barrier" ::: "memory");  // balance the stagger
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every read of both buffers retired
+    }
+    // sched bit 12: half 0 runs its epilogue (and stages the next tile's first K-tiles) while
+    // half 1 is still in MATH(nk-1), and takes the balancing barrier after it.  Both
+    // buffers are free then: every READ segment ends with lgkmcnt(0) before its barrier,
+    // and half 0 has passed the barrier that ends half 1's last READ.  Measured slower
+    // (r7d: fc1 + GELU 190 -> 215 us, fused qkv 151 -> 158 us, aggregator step +1.5 ms).
+    const bool early = (sched >> 12) & 1;
+    if (!early) {
+      if (wm == 0) asm volatile("s_barrier" ::: "memory");  // balance the stagger
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every read of both buffers retired
+    }
 
     // RESID: this tile's fp32 residual rows, loaded BEFORE the next tile's DMA
     // (the compiler's waits for them then never cover the younger DMA)
@@ -1519,11 +1552,21 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
           }
           if constexpr (GELU) {
             // GELU of the bf16 Linear output (autocast), from the LDS table of
-            // torch's float32 GELU rounded to bf16 (gelu_lut.h)
-            a0 = gelu2_lut(a0, lut_s);
-            a1 = gelu2_lut(a1, lut_s);
-            b0 = gelu2_lut(b0, lut_s);
-            b1 = gelu2_lut(b1, lut_s);
+            // torch's float32 GELU rounded to bf16 (gelu_lut.h): the four words'
+            // eight lookups back to back, the out-of-table values (|x| < 2^-16 or
+            // >= 64) re-done on a wave-uniform rare path
+            uint32_t oor = 0;
+            const uint32_t ra0 = a0, ra1 = a1, rb0 = b0, rb1 = b1;
+            a0 = gelu2_clamped(ra0, lut_s, oor);
+            a1 = gelu2_clamped(ra1, lut_s, oor);
+            b0 = gelu2_clamped(rb0, lut_s, oor);
+            b1 = gelu2_clamped(rb1, lut_s, oor);
+            if (__builtin_amdgcn_ballot_w64(oor != 0) != 0) {
+              a0 = gelu2_lut(ra0, lut_s);
+              a1 = gelu2_lut(ra1, lut_s);
+              b0 = gelu2_lut(rb0, lut_s);
+              b1 = gelu2_lut(rb1, lut_s);
+            }
           }
           // rows 1 <-> 0 and 3 <-> 2 of (a = fragment np, b = fragment np+1)
           const auto s0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
@@ -1533,6 +1576,7 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
         }
       }
     }
+    if (early && wm == 0) asm volatile("s_barrier" ::: "memory");  // balance: half 1's MATH(nk-1) ends
     if (!more) break;
     // own K-tile 0 of the next tile landed (K-tile 1 and the stores may still
     // be in flight), then everyone's
@@ -1605,7 +1649,7 @@ int launch_ppp_fk(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, in
     const char* d = getenv("VGGT_GEMM_SPLITDMA");
     return (e ? atoi(e) & 255 : 4) | (d && !atoi(d) ? 0 : 256);
   }();
-  gemm_ppp_kernel<EPI, BMT, FK><<<nwg, PNT, lds, s>>>(a, lda, w, ldw, M, N, K, ep, sched | (g_vggt_gemm_pipe & 7) << 9);
+  gemm_ppp_kernel<EPI, BMT, FK><<<nwg, PNT, lds, s>>>(a, lda, w, ldw, M, N, K, ep, sched | (g_vggt_gemm_pipe & 31) << 9);
   return VGGT_OK;
 }
 
