@@ -1292,6 +1292,11 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
       const bool wall = (sched >> 11) & 1;
       const bool dh0 = (((sched >> 9) & 1) && wm == 0) || wall;
       const bool mh1 = ((sched >> 10) & 1) && wm == 1 && !wall;
+#ifdef VGGT_KO_DMA
+      constexpr bool ko_dma = true;  // diagnostic build only (wrong results): no in-loop DMA
+#else
+      constexpr bool ko_dma = false;
+#endif
       for (int kt = 0; kt < nk; ++kt) {
         const int buf = (b0 + kt) & 1;
         const bool pf = kt >= 1 && kt + 1 < nk;
@@ -1299,7 +1304,8 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
         // The W pieces (read by both wave halves from the next segment on) land
         // before this segment's barrier, the A pieces (read by this half two
         // segments later) before the MATH segment's.
-        if (pf && wall) {
+        if (ko_dma) {
+        } else if (pf && wall) {
           if (wm == 0) {
             stage_w(buf ^ 1, kt + 1);
             stage_w2(buf ^ 1, kt + 1);
@@ -1525,6 +1531,19 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
           __builtin_amdgcn_raw_buffer_store_b128(pk, ro, (ml * (int)ep.ldo + hb + np * 16 + ncol) * 2, 0, 0);
         }
       }
+#ifdef VGGT_KO_EPI
+    } else if (EPI == VGGT_EPI_BF16 || EPI == VGGT_EPI_GELU_BF16) {
+      // diagnostic build only (wrong results): the same NST 16-B stores of raw accumulator bits, no epilogue math
+      const int ncol = (rg & 1) * 16 + (rg >> 1) * 8;
+#pragma unroll
+      for (int np = 0; np < C::NI; np += 2)
+#pragma unroll
+        for (int mi = 0; mi < C::MI; ++mi) {
+          const int ml = wm * C::HM + mi * 16 + (lane & 15);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[np][mi]), ro,
+                                                 (ml * (int)ep.ldo + n0 + wn * C::WN + np * 16 + ncol) * 2, 0, 0);
+        }
+#endif
     } else {
       // after the swap, row group rg holds fragment ni + (rg & 1), features 8 * (rg >> 1) ..
       const int ncol = (rg & 1) * 16 + (rg >> 1) * 8;
