@@ -1289,47 +1289,53 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
       // Bit 11 (with bit 9): half 0 issues every W piece of K-tile kt+1 (its own and half 1's rows,
       // the latter 128 rows on through the scalar offset) and half 1 only its A pieces, which it then
       // waits for at the end of MATH(kt) like half 0 -- no READ segment waits on DMA at all.
-      const bool wall = (sched >> 11) & 1;
-      const bool dh0 = (((sched >> 9) & 1) && wm == 0) || wall;
-      const bool mh1 = ((sched >> 10) & 1) && wm == 1 && !wall;
 #ifdef VGGT_KO_DMA
       constexpr bool ko_dma = true;  // diagnostic build only (wrong results): no in-loop DMA
 #else
       constexpr bool ko_dma = false;
 #endif
-      for (int kt = 0; kt < nk; ++kt) {
-        const int buf = (b0 + kt) & 1;
-        const bool pf = kt >= 1 && kt + 1 < nk;
-        // READ(kt): K-tile kt+1's W pieces, then its A pieces; both K halves' fragments.
-        // The W pieces (read by both wave halves from the next segment on) land
-        // before this segment's barrier, the A pieces (read by this half two
-        // segments later) before the MATH segment's.
-        if (ko_dma) {
-        } else if (pf && wall) {
-          if (wm == 0) {
+      // the default placement (bit 11) as its own copy of the loop, with no runtime
+      // placement branches in it
+      auto fk_loop = [&](auto wallc) {
+        constexpr bool WALL = decltype(wallc)::value;
+        const bool dh0 = WALL || (((sched >> 9) & 1) && wm == 0);
+        const bool mh1 = !WALL && ((sched >> 10) & 1) && wm == 1;
+        for (int kt = 0; kt < nk; ++kt) {
+          const int buf = (b0 + kt) & 1;
+          const bool pf = kt >= 1 && kt + 1 < nk;
+          // READ(kt): K-tile kt+1's DMA pieces, then both K halves' fragments
+          if constexpr (WALL) {
+            if (pf && !ko_dma) {
+              if (wm == 0) {
+                stage_w(buf ^ 1, kt + 1);
+                stage_w2(buf ^ 1, kt + 1);
+              }
+              stage_a(buf ^ 1, kt + 1);
+            }
+          } else if (pf && !mh1 && !ko_dma) {
             stage_w(buf ^ 1, kt + 1);
-            stage_w2(buf ^ 1, kt + 1);
+            stage_a(buf ^ 1, kt + 1);
           }
-          stage_a(buf ^ 1, kt + 1);
-        } else if (pf && !mh1) {
-          stage_w(buf ^ 1, kt + 1);
-          stage_a(buf ^ 1, kt + 1);
+          read_frags(buf, 0);
+          read_frags2(buf);
+          const bool lead = WALL ? !(wm == 1 && kt == 0) : dh0;  // waits move to the end of MATH
+          if (lead) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          else if (!WALL && pf && !mh1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::AL) : "memory");
+          else if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NST) : "memory");
+          else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (WALL) math2();
+          else math2_stage(mh1 && kt + 2 < nk, buf, kt + 2);
+          __builtin_amdgcn_sched_barrier(0);
+          if (lead) {
+            if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NST) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+          } else if (!WALL && pf && !mh1) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+          else asm volatile("s_barrier" ::: "memory");
         }
-        read_frags(buf, 0);
-        read_frags2(buf);
-        if (dh0 && !(wall && wm == 1 && kt == 0)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        else if (pf && !mh1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::AL) : "memory");
-        else if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NST) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        math2_stage(mh1 && kt + 2 < nk, buf, kt + 2);
-        __builtin_amdgcn_sched_barrier(0);
-        if (dh0 && !(wall && wm == 1 && kt == 0)) {
-          if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NST) : "memory");
-          else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        } else if (pf && !mh1) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        else asm volatile("s_barrier" ::: "memory");
-      }
+      };
+      if ((sched >> 11) & 1) fk_loop(std::true_type{});
+      else fk_loop(std::false_type{});
     } else {
     // (sched bit 13; measured slower for the fused qkv GEMM: 147.3-148.6 -> 150.4-151.2 us, r7d)
     const bool wall_h = (sched >> 13) & 1;
@@ -1400,6 +1406,17 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
           rx[ni][mi] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, (ml * (int)ep.ldo + nl) * 4, 0, 0));
         }
     }
+#ifdef VGGT_EPI_BIAS_EARLY
+    // the plain / GELU epilogue's bias values from LDS before the next tile's DMA is issued
+    f32x4 bvs[C::NI];
+    if constexpr (EPI == VGGT_EPI_BF16 || GELU) {
+#pragma unroll
+      for (int ni = 0; ni < C::NI; ++ni) bvs[ni] = *(const f32x4*)(bias_s + n0 + wn * C::WN + ni * 16 + 4 * (lane >> 4));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int ni = 0; ni < C::NI; ++ni) asm volatile("" : "+v"(bvs[ni]));
+    }
+#endif
     // the next tile's K-tiles 0 and 1, in flight during this epilogue
     const int next = tile + gridDim.x;
     const bool more = next < ntiles;
@@ -1553,8 +1570,12 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
       (void)rpre;
 #pragma unroll
       for (int np = 0; np < C::NI; np += 2) {
+#ifdef VGGT_EPI_BIAS_EARLY
+        const f32x4 bv0 = bvs[np], bv1 = bvs[np + 1];
+#else
         const f32x4 bv0 = *(const f32x4*)(bias_s + n0 + wn * C::WN + np * 16 + 4 * rg);
         const f32x4 bv1 = *(const f32x4*)(bias_s + n0 + wn * C::WN + (np + 1) * 16 + 4 * rg);
+#endif
         const int nl = n0 + wn * C::WN + np * 16 + ncol;
 #pragma unroll
         for (int mi = 0; mi < C::MI; ++mi) {
