@@ -1409,7 +1409,7 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
 #ifdef VGGT_EPI_BIAS_EARLY
     // the plain / GELU epilogue's bias values from LDS before the next tile's DMA is issued
     f32x4 bvs[C::NI];
-    if constexpr (EPI == VGGT_EPI_BF16 || GELU) {
+    if constexpr (EPI != VGGT_EPI_F32 && EPI != VGGT_EPI_RESID_F32) {  // (the fused qkv's v block too)
 #pragma unroll
       for (int ni = 0; ni < C::NI; ++ni) bvs[ni] = *(const f32x4*)(bias_s + n0 + wn * C::WN + ni * 16 + 4 * (lane >> 4));
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
