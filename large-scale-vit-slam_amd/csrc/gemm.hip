@@ -1296,8 +1296,9 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
 #endif
       // the default placement (bit 11) as its own copy of the loop, with no runtime
       // placement branches in it
-      auto fk_loop = [&](auto wallc) {
+      auto fk_loop = [&](auto wallc, auto rfc) {
         constexpr bool WALL = decltype(wallc)::value;
+        constexpr bool rfirst = decltype(rfc)::value;
         const bool dh0 = WALL || (((sched >> 9) & 1) && wm == 0);
         const bool mh1 = !WALL && ((sched >> 10) & 1) && wm == 1;
         for (int kt = 0; kt < nk; ++kt) {
@@ -1305,6 +1306,12 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
           const bool pf = kt >= 1 && kt + 1 < nk;
           // READ(kt): K-tile kt+1's DMA pieces, then both K halves' fragments
           if constexpr (WALL) {
+            // sched bit 14: the fragment reads before the DMA issue (the reads then land while
+            // the pieces issue)
+            if constexpr (rfirst) {
+              read_frags(buf, 0);
+              read_frags2(buf);
+            }
             if (pf && !ko_dma) {
               if (wm == 0) {
                 stage_w(buf ^ 1, kt + 1);
@@ -1312,12 +1319,18 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
               }
               stage_a(buf ^ 1, kt + 1);
             }
-          } else if (pf && !mh1 && !ko_dma) {
-            stage_w(buf ^ 1, kt + 1);
-            stage_a(buf ^ 1, kt + 1);
+            if constexpr (!rfirst) {
+              read_frags(buf, 0);
+              read_frags2(buf);
+            }
+          } else {
+            if (pf && !mh1 && !ko_dma) {
+              stage_w(buf ^ 1, kt + 1);
+              stage_a(buf ^ 1, kt + 1);
+            }
+            read_frags(buf, 0);
+            read_frags2(buf);
           }
-          read_frags(buf, 0);
-          read_frags2(buf);
           const bool lead = WALL ? !(wm == 1 && kt == 0) : dh0;  // waits move to the end of MATH
           if (lead) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
           else if (!WALL && pf && !mh1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::AL) : "memory");
@@ -1334,8 +1347,12 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
           else asm volatile("s_barrier" ::: "memory");
         }
       };
-      if ((sched >> 11) & 1) fk_loop(std::true_type{});
-      else fk_loop(std::false_type{});
+      if ((sched >> 11) & 1) {
+        if ((sched >> 14) & 1) fk_loop(std::true_type{}, std::true_type{});
+        else fk_loop(std::true_type{}, std::false_type{});
+      } else {
+        fk_loop(std::false_type{}, std::false_type{});
+      }
     } else {
     // (sched bit 13; measured slower for the fused qkv GEMM: 147.3-148.6 -> 150.4-151.2 us, r7d)
     const bool wall_h = (sched >> 13) & 1;
@@ -1689,7 +1706,7 @@ int launch_ppp_fk(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, in
     const char* d = getenv("VGGT_GEMM_SPLITDMA");
     return (e ? atoi(e) & 255 : 4) | (d && !atoi(d) ? 0 : 256);
   }();
-  gemm_ppp_kernel<EPI, BMT, FK><<<nwg, PNT, lds, s>>>(a, lda, w, ldw, M, N, K, ep, sched | (g_vggt_gemm_pipe & 31) << 9);
+  gemm_ppp_kernel<EPI, BMT, FK><<<nwg, PNT, lds, s>>>(a, lda, w, ldw, M, N, K, ep, sched | (g_vggt_gemm_pipe & 63) << 9);
   return VGGT_OK;
 }
 
