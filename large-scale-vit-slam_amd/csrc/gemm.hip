@@ -1682,7 +1682,11 @@ inline int ppp_pick_bm(int epi, int M, int N) {
   const int cus = cu_count();
   const long r256 = ((long)((M + 255) / 256) * (N / 256) + cus - 1) / cus;
   const long r192 = ((long)((M + 191) / 192) * (N / 256) + cus - 1) / cus;
+#ifdef VGGT_BM_RULE_LE
+  return r192 * 192 * 10 <= r256 * 256 * 9 ? 192 : 256;
+#else
   return r192 * 192 * 10 < r256 * 256 * 9 ? 192 : 256;
+#endif
 }
 
 template <int EPI, int BMT, bool FK>

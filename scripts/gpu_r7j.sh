@@ -25,14 +25,3 @@ for w in "chunk:--workload chunk --steps 5 --warmup 2" "train:--workload train -
   timeout -k 10 400 python3 bench.py $a --no-cpu-baseline > "$OUT/bench_$n.json" 2>> "$OUT/bench_err.log" || exit $?
   echo "$n: $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['ms_per_step'], d['value'])" "$OUT/bench_$n.json")"
 done
-# A/B after the snapshot: the fused qkv GEMM on the whole-K-tile loop (VGGT_GEMM_FULLK=7)
-VGGT_GEMM_FULLK=7 timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
-  tests/test_gpu_kernels.py -k "qkv" > "$OUT/pytest_fk7.log" 2>&1 || { tail -20 "$OUT/pytest_fk7.log"; exit 1; }
-tail -1 "$OUT/pytest_fk7.log"
-for r in 1 2; do
-  for f in 5 7; do
-    VGGT_GEMM_FULLK=$f timeout -k 10 300 python3 bench.py --no-cpu-baseline > "$OUT/fk$f.tmp" 2>> "$OUT/bench_err.log" || exit $?
-    cat "$OUT/fk$f.tmp" >> "$OUT/fk$f.json"
-    echo "fullk $f: $(python3 -c "import json,sys; print(json.load(open(sys.argv[1]))['ms_per_step'])" "$OUT/fk$f.tmp")"
-  done
-done

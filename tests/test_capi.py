@@ -43,3 +43,32 @@ def test_product_refuses_cpu_tensors():
     a = torch.zeros(128, 64, dtype=torch.bfloat16)
     with pytest.raises(RuntimeError, match="HIP devices only"):
         _native.gemm_bf16(a, a, torch.zeros(128), torch.zeros(128, 128, dtype=torch.bfloat16), 0)
+
+
+def test_tune_knobs_range_and_restore():
+    """vggt_tune (a host-side switch, no GPU call) returns the previous value and rejects
+    values outside each knob's documented range (include/vggt_mi355x.h)."""
+    from aligned_vggt import _native as N
+    if not os.path.exists(N.LIB_PATH):
+        pytest.skip("library not built")
+    lib = N.lib()
+    for knob, good, bad in ((N.TUNE_GEMM_PIPE, (0, 1, 5, 37, 63), (-1, 64)),
+                            (N.TUNE_ATTN16, (0, 1, 2), (3, -1)),
+                            (N.TUNE_ATTN_WAVES, (2, 4, 8), (3, 16))):
+        first = lib.vggt_tune(knob, good[0])
+        assert first >= 0
+        prev = good[0]
+        for v in good[1:]:
+            assert lib.vggt_tune(knob, v) == prev
+            prev = v
+        for v in bad:
+            assert lib.vggt_tune(knob, v) < 0
+            assert lib.vggt_tune(knob, prev) == prev  # a rejected value changed nothing
+        lib.vggt_tune(knob, first)
+    # the defaults the round-3 measurements chose (DESIGN.md §4.1 / §4.2), unless the environment overrides them
+    if "VGGT_GEMM_PIPE" not in os.environ:
+        p = lib.vggt_tune(N.TUNE_GEMM_PIPE, 5)
+        assert p == 5
+    if "VGGT_ATTN16" not in os.environ:
+        p = lib.vggt_tune(N.TUNE_ATTN16, 2)
+        assert p == 2
