@@ -580,9 +580,9 @@ __global__ __launch_bounds__(NT, 2) void conv_pre_kernel(ConvArgs a, const bf16_
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < NTN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto compute = [&](int cur) {
+  bf16x8 ah[4], al[4], bh[NTN], bl[NTN];
+  auto reads = [&](int cur) {
     const char* base = smem + cur * STG;
-    bf16x8 ah[4], al[4], bh[NTN], bl[NTN];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       const int o = (wm * 64 + mt * 16) * 64 + roff;
@@ -595,6 +595,8 @@ __global__ __launch_bounds__(NT, 2) void conv_pre_kernel(ConvArgs a, const bf16_
       bh[nt] = *(const bf16x8*)(base + 2 * AT + o);
       bl[nt] = *(const bf16x8*)(base + 2 * AT + WT + o);
     }
+  };
+  auto mfmas = [&]() {
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
@@ -610,8 +612,15 @@ __global__ __launch_bounds__(NT, 2) void conv_pre_kernel(ConvArgs a, const bf16_
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
+#ifdef VGGT_CONV_STAGE_LATE
+    // (diagnostic variant) this step's fragment reads first, the next step's DMA issue while they land
+    reads(cur);
     if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
-    compute(cur);
+#else
+    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+    reads(cur);
+#endif
+    mfmas();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
