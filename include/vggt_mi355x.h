@@ -66,7 +66,8 @@ const char* vggt_version(void);
                                     K-tile at the end of MATH, 2 half 1 stages K-tile kt+2 inside MATH(kt),
                                     4 half 0 issues every W piece, no READ waits on DMA,
                                     8 half 0's epilogue overlaps half 1's last MATH segment, 16 bit 4 in the
-                                    half-K loop, 32 fragment reads before the DMA issue; default 5 */
+                                    half-K loop, 32 fragment reads before the DMA issue, 64 half 1 issues its W pieces
+                                    after its MFMAs; default 5 */
 int vggt_tune(int knob, int value);
 
 /*

@@ -61,7 +61,7 @@ extern "C" int vggt_tune(int knob, int value) {
       g_vggt_conv_pf2 = value;
       return prev;
     case VGGT_TUNE_GEMM_PIPE:
-      if (value < 0 || value > 63) return VGGT_ERR_UNSUPPORTED;
+      if (value < 0 || value > 127) return VGGT_ERR_UNSUPPORTED;
       prev = g_vggt_gemm_pipe;
       g_vggt_gemm_pipe = value;
       return prev;

@@ -1347,7 +1347,40 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
           else asm volatile("s_barrier" ::: "memory");
         }
       };
-      if ((sched >> 11) & 1) {
+      // sched bit 15: half 0 issues its own W and A pieces of K-tile kt+1 at READ(kt) and waits for them at
+      // the end of MATH(kt); half 1 issues its W pieces of K-tile j+2 after the MFMAs of MATH(j) (the buffer
+      // of K-tile j is free by then) and its A pieces of K-tile kt+1 at READ(kt), and waits for the W pieces
+      // at the end of READ(kt) -- a segment after issue -- and for the A pieces at the end of MATH(kt).  Each
+      // READ segment issues at most eight pieces instead of half 0's twelve.
+      auto fk_w1m = [&]() {
+        for (int kt = 0; kt < nk; ++kt) {
+          const int buf = (b0 + kt) & 1;
+          const bool pf = kt >= 1 && kt + 1 < nk;
+          if (pf && !ko_dma) {
+            if (wm == 0) stage_w(buf ^ 1, kt + 1);
+            stage_a(buf ^ 1, kt + 1);
+          }
+          read_frags(buf, 0);
+          read_frags2(buf);
+          if (wm == 0) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          else if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NST) : "memory");
+          else if (pf) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::AL) : "memory");
+          else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          math2();
+          __builtin_amdgcn_sched_barrier(0);
+          const bool w1 = wm == 1 && kt + 2 < nk && !ko_dma;
+          if (w1) stage_w(buf, kt + 2);
+          if (wm == 0) {
+            if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NST) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+          } else if (w1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(C::WL) : "memory");
+          else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+      };
+      if ((sched >> 15) & 1) {
+        fk_w1m();
+      } else if ((sched >> 11) & 1) {
         if ((sched >> 14) & 1) fk_loop(std::true_type{}, std::true_type{});
         else fk_loop(std::true_type{}, std::false_type{});
       } else {
@@ -1710,7 +1743,7 @@ int launch_ppp_fk(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, in
     const char* d = getenv("VGGT_GEMM_SPLITDMA");
     return (e ? atoi(e) & 255 : 4) | (d && !atoi(d) ? 0 : 256);
   }();
-  gemm_ppp_kernel<EPI, BMT, FK><<<nwg, PNT, lds, s>>>(a, lda, w, ldw, M, N, K, ep, sched | (g_vggt_gemm_pipe & 63) << 9);
+  gemm_ppp_kernel<EPI, BMT, FK><<<nwg, PNT, lds, s>>>(a, lda, w, ldw, M, N, K, ep, sched | (g_vggt_gemm_pipe & 127) << 9);
   return VGGT_OK;
 }
 

@@ -52,7 +52,7 @@ def test_tune_knobs_range_and_restore():
     if not os.path.exists(N.LIB_PATH):
         pytest.skip("library not built")
     lib = N.lib()
-    for knob, good, bad in ((N.TUNE_GEMM_PIPE, (0, 1, 5, 37, 63), (-1, 64)),
+    for knob, good, bad in ((N.TUNE_GEMM_PIPE, (0, 1, 5, 37, 64, 127), (-1, 128)),
                             (N.TUNE_ATTN16, (0, 1, 2), (3, -1)),
                             (N.TUNE_ATTN_WAVES, (2, 4, 8), (3, 16))):
         first = lib.vggt_tune(knob, good[0])
