@@ -528,3 +528,37 @@ def test_attention16_accuracy_matches_32x32(N, batch, n, H):
     print("rel-L2 vs fp64:", errs)
     assert errs[161] < 5e-3 and errs[33] < 5e-3, errs
     assert errs[161] <= 1.1 * errs[33] + 1e-5, errs
+
+
+@pytest.mark.parametrize("Nn,K,epi,M", [(4096, 1024, 1, 5000), (1024, 4096, 0, 21984), (3072, 1024, 0, 1000),
+                                        (1024, 1024, 2, 6592)])
+def test_gemm_dma_placements_bitwise(N, Nn, K, epi, M):
+    """Every DMA placement of the persistent GEMM's K loop (VGGT_TUNE_GEMM_PIPE) computes the same
+    bits as the default: placement moves loads and waits, never the arithmetic.  Ragged M, whole-K (bf16 / GELU /
+    residual) loops."""
+    torch.manual_seed(7)
+    dev = torch.device("cuda:0")
+    a = ((torch.rand(M, K, device=dev) * 2 - 1)).bfloat16()
+    w = ((torch.rand(Nn, K, device=dev) * 2 - 1) * K ** -0.5).bfloat16()
+    b = torch.randn(Nn, device=dev) * 0.1
+    g = torch.rand(Nn, device=dev)
+    x0 = torch.randn(M, Nn, device=dev)
+
+    def run(pipe):
+        prev = N.tune(N.TUNE_GEMM_PIPE, pipe)
+        try:
+            if epi == 2:
+                out = x0.clone()
+                N.gemm_bf16(a, w, b, out, epi, gamma=g)
+            else:
+                out = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
+                N.gemm_bf16(a, w, b, out, epi)
+            torch.cuda.synchronize()
+            return out
+        finally:
+            N.tune(N.TUNE_GEMM_PIPE, prev)
+
+    ref = run(5)
+    assert torch.isfinite(ref.float()).all()
+    for pipe in (0, 1, 2, 3, 13, 16, 37, 64):
+        assert torch.equal(run(pipe), ref), pipe
