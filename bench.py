@@ -375,6 +375,10 @@ def bench_full(args, world, rank, dev):
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
+    recurrence = None
+    if args.workload == "sequence":
+        recurrence = _recurrence_probe(pipe, step, n_chunks_step, dt / args.steps * 1e3, world)
+    if world > 1:
         dist.destroy_process_group()
     if rank == 0:
         value = n_chunks_step * args.steps / dt
@@ -389,8 +393,46 @@ def bench_full(args, world, rank, dev):
                                             "image": [H, W], "heads": "camera+depth+alignment(memory %d)" % nm,
                                             "parallelism": ("chunk pipeline x%d (RCCL baton ring)" % world
                                                             if args.workload == "sequence" else
-                                                            "replicas x%d" % world)}}),
+                                                            "replicas x%d" % world)},
+            "recurrence": recurrence}),
               flush=True)
+
+
+def _recurrence_probe(pipe, step, n_chunks, t1_ms, world):
+    """The alignment recurrence's critical path: chunk i's
+    alignment needs chunk i-1's post-head tokens, so with W ranks a sequence
+    takes at least n_chunks x t_align (+ W-1 .. n-1 baton hops) whatever the
+    encodes do.  Measured after the timed region with HIP events around every
+    align_chunk on its own stream: (a) the sequential schedule (align between
+    encodes on the compute stream: t_align alone) and (b) the ring's schedule
+    (align on the side stream while the next encode group runs: t_align under
+    load, the regime of every W > 1 rank).  At W = 1 (b) is the W = 1 ring
+    schedule (overlap_align), whose sequence time is reported beside."""
+    import statistics
+    pipe.time_align = True
+    out = {"n_chunks": n_chunks}
+    modes = (("alone", False), ("under_load", True)) if world == 1 else (("under_load", None),)
+    for name, ov_mode in modes:
+        keep = pipe.overlap_align
+        if ov_mode is not None:
+            pipe.overlap_align = ov_mode
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) * 1e3
+        pipe.overlap_align = keep
+        ms = pipe.align_ms()
+        out["t_align_ms_%s_median" % name] = round(statistics.median(ms), 3) if ms else None
+        out["t_align_ms_%s_max" % name] = round(max(ms), 3) if ms else None
+        out["sequence_ms_%s" % name] = round(wall, 1)
+    pipe.time_align = False
+    t_load = out.get("t_align_ms_under_load_median")
+    if t_load and world == 1:
+        out["T8_lower_bound_ms"] = round(n_chunks * t_load, 1)
+        out["T1_over_8_ms"] = round(t1_ms / 8, 1)
+        out["bound_frac_of_T1_over_8"] = round(n_chunks * t_load / (t1_ms / 8), 3)
+    return out
 
 
 def bench_train(args, world, rank, dev):

@@ -368,12 +368,27 @@ def linear_f32(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], o
 _SPLIT_WS = {}
 
 
+def _stream_key(device) -> tuple:
+    """(device, current stream id): scratch is reused in stream order only, so
+    work queued on two streams at once (the ring aligns chunk i on a side
+    stream while the compute stream encodes, dist/pipeline.py) never shares a
+    slab -- and a grown slab's old storage is released on the one stream that
+    used it (the caching allocator's reuse is ordered on that stream)."""
+    device = torch.device(device)
+    if device.type != "cuda":
+        return (device, 0)
+    if device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    return (device, torch.cuda.current_stream(device).stream_id)
+
+
 def _split_ws(device, n_floats: int) -> torch.Tensor:
-    """Grow-only per-device scratch for split-K partial sums (stream-ordered reuse)."""
-    t = _SPLIT_WS.get(device)
+    """Grow-only per-(device, stream) scratch for split-K partial sums."""
+    key = _stream_key(device)
+    t = _SPLIT_WS.get(key)
     if t is None or t.numel() < n_floats:
-        t = torch.empty(n_floats, device=device, dtype=torch.float32)
-        _SPLIT_WS[device] = t
+        t = torch.empty(n_floats, device=key[0], dtype=torch.float32)
+        _SPLIT_WS[key] = t
     return t
 
 
@@ -612,12 +627,14 @@ _TRAIN_WS = {}
 
 
 def _train_ws(device, nbytes: int) -> torch.Tensor:
-    """Grow-only per-device scratch for the deterministic reduction partials
-    (stream-ordered reuse: every user consumes it before the next launch)."""
-    t = _TRAIN_WS.get(device)
+    """Grow-only per-(device, stream) scratch for the deterministic reduction
+    partials (stream-ordered reuse: every user consumes it before the next
+    launch on the same stream; see _stream_key)."""
+    key = _stream_key(device)
+    t = _TRAIN_WS.get(key)
     if t is None or t.numel() * 4 < nbytes:
-        t = torch.empty((nbytes + 3) // 4 + 64, device=device, dtype=torch.float32)
-        _TRAIN_WS[device] = t
+        t = torch.empty((nbytes + 3) // 4 + 64, device=key[0], dtype=torch.float32)
+        _TRAIN_WS[key] = t
     return t
 
 

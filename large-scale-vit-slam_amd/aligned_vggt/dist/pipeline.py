@@ -23,8 +23,9 @@ with point-to-point send/recv: one hop per chunk boundary over one xGMI link
 (~0.2 ms), hidden behind the next chunk's encode.  Each rank interleaves
 encode(own chunk k) -> align(own chunk k) so that, with align << encode, the
 baton ring never stalls an encode.  At the end the small per-chunk outputs
-(pose encodings, Sim(3)/SE(3) alignments) are all-gathered; dense maps (depth,
-points) stay on the rank that produced them unless ``gather_dense``.
+(pose encodings, Sim(3)/SE(3) alignments) reach every rank through one
+fixed-shape ``all_gather_into_tensor`` (RCCL over xGMI); dense depth maps stay
+on the rank that produced them unless ``gather_dense`` (a second all-gather).
 """
 from __future__ import annotations
 
@@ -157,8 +158,17 @@ class ChunkPipeline:
     (FeatureAlignedVGGT does) and be replicated on every rank."""
 
     def __init__(self, model, group=None, device=None, gather_dense: bool = False,
-                 encode_group: Optional[int] = None):
+                 encode_group: Optional[int] = None, overlap_align: Optional[bool] = None,
+                 time_align: bool = False):
         self.model = model
+        # one rank: align chunk i on the side stream while the next encode group
+        # runs (the ring's schedule with the baton kept on the device);
+        # VGGT_OVERLAP_ALIGN=1 sets the default.  time_align: HIP events around
+        # every align_chunk on its stream (align_ms()).
+        if overlap_align is None:
+            overlap_align = os.environ.get("VGGT_OVERLAP_ALIGN", "0") == "1"
+        self.overlap_align = overlap_align
+        self.time_align = time_align
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -254,14 +264,15 @@ class ChunkPipeline:
             memory_shape=None) -> Optional[dict]:
         """images: (B, N, 3, H, W) (any device; each rank moves only its
         chunks).  token_dims = (P+1, C) of the alignment head's tokens;
-        memory_shape = (B, n_mem, dec) or None.  Returns merged predictions on
-        rank 0 (pose_enc (B,N,9), chunk_sim3_alignment_enc (B,n_chunks,8),
-        frame_se3_alignment_enc (B,sum(S_i-1),7), and depth/points if gathered),
-        None elsewhere."""
+        memory_shape = (B, n_mem, dec) or None.  Returns the merged predictions
+        on every rank (pose_enc (B,N,9), chunk_sim3_alignment_enc (B,n_chunks,8),
+        frame_se3_alignment_enc (B,sum(S_i-1),7), and depth if gathered)."""
         B, Nf = images.shape[:2]
+        self._img_hw = tuple(images.shape[-2:])
         chunks = generate_chunks(Nf, "chunk_overlap", chunk_width, num_overlap)
         keys = ["overlap_tokens", "pose_enc"] + (["memory_tokens"] if memory_shape is not None else [])
-        if self.world == 1:
+        self.align_events = []
+        if self.world == 1 and not self.overlap_align:
             mine = self._run_local(images, chunks, num_overlap, keys, memory_shape, B)
         else:
             mine = self._run_ring(images, chunks, num_overlap, keys, token_dims, memory_shape, B)
@@ -315,19 +326,33 @@ class ChunkPipeline:
                 nxt = fetch(groups[gi]) if gi < len(groups) else None
                 encs.update(self._encode(images, chunks, g, frames))
             ctx = self._ctx_from(local, B, memory_shape) if i > 0 else None
+            ev0 = self._tick()
             pred = self.model.align_chunk(encs.pop(i), num_overlap, ctx)
+            if ev0 is not None:
+                self.align_events.append((i, ev0, self._tick()))
             if i + 1 < n:
                 local = {k: (pred[k][-1] if isinstance(pred[k], list) else pred[k]) for k in keys}
             mine[i] = self._summary(pred, len(chunks[i]))
         return mine
 
     def _run_ring(self, images, chunks, num_overlap, keys, token_dims, memory_shape, B) -> Dict[int, dict]:
-        """W > 1 ranks: rank r owns chunks r, r + W, ...  Encodes run on the
-        compute stream one group ahead; each alignment runs on a side stream
+        """Rank r owns chunks r, r + W, ...  Encodes run on the compute stream
+        one group ahead; each alignment runs on a high-priority side stream
         that waits (device-side) for its encode and for the baton from rank
-        i - 1 (irecv posted early), and posts the baton to rank i + 1 (isend)
-        as soon as it is done -- the host never blocks on a peer, and the
-        compute stream keeps encoding while a baton is in flight."""
+        i - 1, and posts the baton to rank i + 1 (isend) as soon as it is
+        done -- the host never blocks on a peer, and the compute stream keeps
+        encoding while a baton is in flight.
+
+        The baton's irecv is posted on the side stream BEFORE the side stream
+        waits for the chunk's encode: RCCL orders its communication stream
+        after the stream current at the call, so the receive can land while
+        the encode still runs (posted after the wait it could not start until
+        the encode had finished).  Under gloo ``w.wait()`` blocks the host
+        instead, which only orders the launches.
+
+        W == 1 (``overlap_align``): the same schedule on one GPU with the baton
+        kept on the device -- chunk i aligns on the side stream while the next
+        encode group runs on the compute stream."""
         W, r = self.world, self.rank
         n = len(chunks)
         P1, C = token_dims
@@ -360,6 +385,7 @@ class ChunkPipeline:
 
         mine: Dict[int, dict] = {}
         sends = []
+        local = None
         for i in own:
             gi = group_of[i]
             while enqueued <= min(gi + 1, len(groups) - 1):  # this group and the next one queued
@@ -367,20 +393,31 @@ class ChunkPipeline:
                 enqueued += 1
             enc = encs.pop(i)
             with (torch.cuda.stream(side) if cuda else contextlib.nullcontext()):
-                if cuda:
-                    side.wait_event(ready.pop(i))
-                    _record_stream(enc, side)
                 ctx = None
-                if i > 0:
+                works = ()
+                if i > 0 and W > 1:
                     Sp = len(chunks[i - 1])
                     works, ctx_in = self._irecv((i - 1) % W, self._baton_shapes(
                         B, Sp, _overlap_of(Sp, num_overlap), P1, C, memory_shape))
-                    for w in works:
-                        w.wait()  # RCCL: the side stream waits; gloo: the host does
+                if cuda:
+                    side.wait_event(ready.pop(i))
+                    _record_stream(enc, side)
+                if i > 0:
+                    if W > 1:
+                        for w in works:
+                            w.wait()  # RCCL: the side stream waits; gloo: the host does
+                    else:
+                        ctx_in = local
                     ctx = self._ctx_from(ctx_in, B, memory_shape)
+                ev0 = self._tick()
                 pred = self.model.align_chunk(enc, num_overlap, ctx)
+                if ev0 is not None:
+                    self.align_events.append((i, ev0, self._tick()))
                 if i + 1 < n:
-                    sends.append(self._isend(pred, (i + 1) % W, keys))
+                    if W > 1:
+                        sends.append(self._isend(pred, (i + 1) % W, keys))
+                    else:
+                        local = {k: (pred[k][-1] if isinstance(pred[k], list) else pred[k]) for k in keys}
                 mine[i] = self._summary(pred, len(chunks[i]))
         for works, _ in sends:
             for w in works:
@@ -391,34 +428,33 @@ class ChunkPipeline:
                 _record_stream(v, main)
         return mine
 
+    def _tick(self):
+        """A timing event on the current stream (``time_align`` on a HIP device), else None."""
+        if not self.time_align or self.device is None or torch.device(self.device).type != "cuda":
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(self.device))
+        return ev
+
+    def align_ms(self) -> List[float]:
+        """Per-chunk alignment time (ms, HIP events on the align stream) of the
+        last ``run`` with ``time_align`` set; synchronises."""
+        out = []
+        for _, a, b in getattr(self, "align_events", []):
+            b.synchronize()
+            out.append(a.elapsed_time(b))
+        return out
+
     def _gather(self, mine: Dict[int, dict], chunks: List[List[int]], num_overlap: int, B: int) -> Optional[dict]:
+        """Every chunk's small outputs (pose encodings, chunk Sim(3), frame
+        SE(3); depth maps with ``gather_dense``) on every rank: ONE fixed-shape
+        ``all_gather_into_tensor`` per kind (RCCL over xGMI).  Rank r's block
+        holds its own chunks r, r + W, ... in slot order, each padded to the
+        longest chunk; chunk i is slot i // W of rank i % W's block."""
         n = len(chunks)
         W = self.world
-        dense = self.gather_dense and any("depth" in v for v in mine.values())
         if W > 1:
-            # every chunk's small outputs -> rank 0 (fixed, known shapes)
-            per_chunk = {}
-            for i in range(n):
-                owner = i % W
-                S = len(chunks[i])
-                shp = {"pose_enc": (B, S, 9), "chunk_sim3": (B, 1, 8), "frame_se3": (B, S - 1, 7)}
-                if dense:
-                    H, Wd = next(iter(mine.values()))["depth"].shape[2:4] if mine else (0, 0)
-                    shp["depth"] = (B, S, H, Wd, 1)
-                    shp["depth_conf"] = (B, S, H, Wd)
-                if owner == self.rank and self.rank == 0:
-                    per_chunk[i] = mine[i]
-                elif owner == self.rank:
-                    for k in shp:
-                        dist.send(mine[i][k].contiguous().to(self.device), 0, group=self.group)
-                elif self.rank == 0:
-                    per_chunk[i] = {}
-                    for k, s in shp.items():
-                        t = torch.empty(s, device=self.device)
-                        dist.recv(t, owner, group=self.group)
-                        per_chunk[i][k] = t
-            if self.rank != 0:
-                return None
+            per_chunk = self._all_gather_chunks(mine, chunks, B)
         else:
             per_chunk = mine
         ov = num_overlap
@@ -431,3 +467,57 @@ class ChunkPipeline:
             out["depth"] = torch.cat([per_chunk[i]["depth"][:, (ov if i > 0 else 0):] for i in range(n)], 1)
             out["depth_conf"] = torch.cat([per_chunk[i]["depth_conf"][:, (ov if i > 0 else 0):] for i in range(n)], 1)
         return out
+
+    def _all_gather_chunks(self, mine: Dict[int, dict], chunks: List[List[int]], B: int) -> Dict[int, dict]:
+        W, r = self.world, self.rank
+        n = len(chunks)
+        slots = (n + W - 1) // W
+        smax = max(len(c) for c in chunks)
+        dev = self.device if self.device is not None else torch.device("cpu")
+        # small outputs, per slot: [has_depth, pose_enc B*smax*9, chunk_sim3 B*8, frame_se3 B*(smax-1)*7]
+        seg = (1, B * smax * 9, B * 8, B * (smax - 1) * 7)
+        per = sum(seg)
+        buf = torch.zeros(slots, per, device=dev, dtype=torch.float32)
+        for j in range(slots):
+            i = r + j * W
+            if i >= n:
+                continue
+            S, m = len(chunks[i]), mine[i]
+            o = seg[0]
+            buf[j, 0] = float(self.gather_dense and "depth" in m)
+            buf[j, o:o + B * S * 9] = m["pose_enc"].reshape(-1)
+            o += seg[1]
+            buf[j, o:o + B * 8] = m["chunk_sim3"].reshape(-1)
+            o += seg[2]
+            buf[j, o:o + B * (S - 1) * 7] = m["frame_se3"].reshape(-1)
+        allb = torch.empty(W * slots, per, device=dev, dtype=torch.float32)
+        dist.all_gather_into_tensor(allb, buf, group=self.group)
+        per_chunk: Dict[int, dict] = {}
+        for i in range(n):
+            row = allb[(i % W) * slots + i // W]
+            S = len(chunks[i])
+            o = seg[0]
+            per_chunk[i] = {"pose_enc": row[o:o + B * S * 9].view(B, S, 9)}
+            o += seg[1]
+            per_chunk[i]["chunk_sim3"] = row[o:o + B * 8].view(B, 1, 8)
+            o += seg[2]
+            per_chunk[i]["frame_se3"] = row[o:o + B * (S - 1) * 7].view(B, S - 1, 7)
+        # every rank sees every chunk's flag, so all agree on the dense collective
+        if bool((allb[:, 0] > 0).any()) and all(float(allb[(i % W) * slots + i // W, 0]) > 0 for i in range(n)):
+            H, Wd = self._img_hw
+            pix = H * Wd
+            d = torch.zeros(slots, 2, B * smax * pix, device=dev, dtype=torch.float32)
+            for j in range(slots):
+                i = r + j * W
+                if i < n:
+                    S = len(chunks[i])
+                    d[j, 0, :B * S * pix] = mine[i]["depth"].reshape(-1)
+                    d[j, 1, :B * S * pix] = mine[i]["depth_conf"].reshape(-1)
+            alld = torch.empty(W * slots, 2, B * smax * pix, device=dev, dtype=torch.float32)
+            dist.all_gather_into_tensor(alld, d, group=self.group)
+            for i in range(n):
+                row = alld[(i % W) * slots + i // W]
+                S = len(chunks[i])
+                per_chunk[i]["depth"] = row[0, :B * S * pix].view(B, S, H, Wd, 1)
+                per_chunk[i]["depth_conf"] = row[1, :B * S * pix].view(B, S, H, Wd)
+        return per_chunk

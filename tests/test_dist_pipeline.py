@@ -32,10 +32,8 @@ def _worker(rank, world, port, Nf, w, ov, q, group=None):
         images = torch.rand(2, Nf, 3, 4, 5, generator=g)
         out = ChunkPipeline(ToyAlignModel(), device=torch.device("cpu"), gather_dense=True, encode_group=group).run(
             images, w, ov, token_dims=(P1, C), memory_shape=(2, NMEM, DEC))
-        if rank == 0:
-            q.put({k: v.clone() for k, v in out.items()})
-        else:
-            assert out is None
+        # the end-of-sequence all-gather leaves the merged outputs on every rank
+        q.put((rank, {k: v.numpy().copy() for k, v in out.items()}))  # by value: the worker may exit first
     finally:
         dist.destroy_process_group()
 
@@ -48,10 +46,14 @@ def _sequential(Nf, w, ov):
 
 @pytest.mark.parametrize("world,Nf,w,ov,group", [(2, 14, 5, 1, None), (2, 64, 16, 4, None), (3, 23, 6, 2, None),
                                                  (4, 40, 8, 3, None), (2, 44, 6, 2, 1), (2, 44, 6, 2, 2),
-                                                 (3, 60, 6, 2, 3)])
+                                                 (3, 60, 6, 2, 3), (5, 9, 5, 1, None),
+                                                 # BASELINE configs[3]/[4] chunking: 512 frames, w16 / ov4 ->
+                                                 # 43 chunks (a tail of 8) over 8 ranks
+                                                 (8, 512, 16, 4, None)])
 def test_pipeline_matches_sequential_loop(world, Nf, w, ov, group):
-    """W ranks (isend/irecv baton ring, alignment on its own stream on GPUs),
-    incl. grouped encodes of each rank's own consecutive chunks."""
+    """W ranks (isend/irecv baton ring, alignment on its own stream on GPUs,
+    all_gather_into_tensor at the end), incl. grouped encodes of each rank's
+    own consecutive chunks and a world larger than the chunk count."""
     ref = _sequential(Nf, w, ov)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -59,13 +61,15 @@ def test_pipeline_matches_sequential_loop(world, Nf, w, ov, group):
     procs = [ctx.Process(target=_worker, args=(r, world, port, Nf, w, ov, q, group)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=120)
+    outs = dict(q.get(timeout=180) for _ in range(world))
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    for k in ("pose_enc", "chunk_sim3_alignment_enc", "frame_se3_alignment_enc", "depth", "depth_conf"):
-        assert got[k].shape == ref[k].shape, k
-        torch.testing.assert_close(got[k], ref[k], rtol=0, atol=0)
+    assert sorted(outs) == list(range(world))
+    for r, got in outs.items():
+        for k in ("pose_enc", "chunk_sim3_alignment_enc", "frame_se3_alignment_enc", "depth", "depth_conf"):
+            assert got[k].shape == tuple(ref[k].shape), (r, k)
+            torch.testing.assert_close(torch.from_numpy(got[k]), ref[k], rtol=0, atol=0)
 
 
 def test_pipeline_single_rank_matches_sequential_loop():
@@ -75,6 +79,18 @@ def test_pipeline_single_rank_matches_sequential_loop():
     got = ChunkPipeline(ToyAlignModel(), device=torch.device("cpu")).run(images, 6, 2, token_dims=(P1, C),
                                                                           memory_shape=(2, NMEM, DEC))
     for k in ("pose_enc", "chunk_sim3_alignment_enc", "frame_se3_alignment_enc", "depth"):
+        torch.testing.assert_close(got[k], ref[k], rtol=0, atol=0)
+
+
+def test_pipeline_single_rank_overlapped_schedule_matches_sequential_loop():
+    """W = 1 with the ring's schedule (align on the side stream while the next
+    encode group runs, baton kept locally): same results as the loop."""
+    ref = _sequential(23, 6, 2)
+    g = torch.Generator().manual_seed(0)
+    images = torch.rand(2, 23, 3, 4, 5, generator=g)
+    got = ChunkPipeline(ToyAlignModel(), device=torch.device("cpu"), gather_dense=True, encode_group=2,
+                        overlap_align=True).run(images, 6, 2, token_dims=(P1, C), memory_shape=(2, NMEM, DEC))
+    for k in ("pose_enc", "chunk_sim3_alignment_enc", "frame_se3_alignment_enc", "depth", "depth_conf"):
         torch.testing.assert_close(got[k], ref[k], rtol=0, atol=0)
 
 

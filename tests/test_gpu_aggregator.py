@@ -41,26 +41,34 @@ def test_aggregator_small_depth(cuda):
         assert o.shape == r.shape
         assert torch.isfinite(o).all()
         e, e32 = _rel(o, r), _rel(r32, r)
+        print("aggregator small depth: hip vs bf16 oracle %.3e, oracle fp32 vs bf16 %.3e" % (e, e32))
         assert e < 2e-2, (e, e32)
 
 
 def test_aggregator_full_depth_two_frames(cuda):
     """Full 24+24 layer aggregator on a 2-frame 112x112 chunk (layers 4,11,17,23)."""
     outs, ref, ref32 = _run(cuda, depth=24, dino_depth=24, B=1, S=2, H=112, W=112, keep=(4, 11, 17, 23))
-    for o, r in zip(outs, ref):
+    for o, r, r32 in zip(outs, ref, ref32):
         assert torch.isfinite(o).all()
-        assert _rel(o, r) < 3e-2, _rel(o, r)
+        e, e32 = _rel(o, r), _rel(r32, r)
+        print("aggregator full depth: hip vs bf16 oracle %.3e, oracle fp32 vs bf16 %.3e" % (e, e32))
+        assert e < 3e-2, (e, e32)
 
 
 def test_aggregator_batch2(cuda):
-    outs, ref, _ = _run(cuda, depth=2, dino_depth=1, B=2, S=2, H=42, W=56, keep=(1,))
-    assert _rel(outs[0], ref[0]) < 2e-2
+    outs, ref, ref32 = _run(cuda, depth=2, dino_depth=1, B=2, S=2, H=42, W=56, keep=(1,))
+    e, e32 = _rel(outs[0], ref[0]), _rel(ref32[0], ref[0])
+    print("aggregator batch 2: hip vs bf16 oracle %.3e, oracle fp32 vs bf16 %.3e" % (e, e32))
+    assert e < 2e-2, (e, e32)
 
 
 def test_aggregator_fused_add_ln_matches_epilogue_path(cuda, monkeypatch):
-    """fc2 as plain GEMM + fused residual-add / next-norm1 pass (default) vs the
-    fp32 read-modify-write epilogue + separate LayerNorm: same arithmetic, so
-    the kept-layer outputs agree to fp32 accumulation-order noise."""
+    """proj / fc2 as plain GEMMs + the fused residual-add / next-LayerNorm row
+    passes (mode 3, the default from 16,384 token rows) vs the fp32
+    read-modify-write epilogues + separate LayerNorms: same arithmetic, so the
+    kept-layer outputs agree to fp32 accumulation-order noise.  The row
+    threshold is lowered so this 3 x 8 x 9 chunk takes the fused path; a
+    launch counter proves each arm ran the path it claims."""
     from aligned_vggt.backbone import layers as L
     from aligned_vggt.backbone.aggregator import Aggregator
     from aligned_vggt.utils.synthetic import synthetic_init_, synthetic_images
@@ -68,11 +76,26 @@ def test_aggregator_fused_add_ln_matches_epilogue_path(cuda, monkeypatch):
     synthetic_init_(agg, seed=5)
     agg = agg.to(cuda)
     img = synthetic_images(1, 3, 112, 126).to(cuda)
-    monkeypatch.setattr(L, "_FUSED_ADD_LN", True)
+    calls = {"n": 0}
+    real = L.N.resid_add_layernorm
+
+    def counted(*a, **k):
+        calls["n"] += 1
+        return real(*a, **k)
+
+    monkeypatch.setattr(L.N, "resid_add_layernorm", counted)
+    monkeypatch.setattr(L, "_FUSED_ADD_LN_MIN_ROWS", 0)
+    monkeypatch.setattr(L, "_FUSED_ADD_LN", 3)
     a, _ = agg(img, keep_layers=(0, 3))
     a = [t.clone() for t in a]
-    monkeypatch.setattr(L, "_FUSED_ADD_LN", False)
+    n_fused = calls["n"]
+    monkeypatch.setattr(L, "_FUSED_ADD_LN", 0)
     b, _ = agg(img, keep_layers=(0, 3))
     torch.cuda.synchronize()
+    # 3 DINOv2 + 4 frame + 4 global blocks, two row passes each (proj and fc2)
+    assert n_fused == 2 * (3 + 4 + 4), n_fused
+    assert calls["n"] == n_fused  # the epilogue arm never took the row pass
     for u, v in zip(a, b):
-        assert _rel(u, v) < 2e-3, _rel(u, v)
+        e = _rel(u, v)
+        print("fused add+LN vs RMW epilogue rel-L2 %.3e" % e)
+        assert e < 2e-3, e

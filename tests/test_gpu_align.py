@@ -132,3 +132,50 @@ def test_point_aligned_two_chunks_vs_oracle(point_model):
             e_hip, e_ref = _rel(a, b), _rel(c, b)
             print(k, e_hip, e_ref)
             assert e_hip < max(3e-2, 1.5 * e_ref), (k, e_hip, e_ref)
+
+
+def test_point_aligned_config0_full_size_two_chunks(N):
+    """BASELINE configs[0] at its size: 8-frame 518 x 518 chunks through the
+    point-aligned VGGT (pointAligned_wrapped_vggt.py:34-157), reduced depth
+    (4 frame/global blocks, 1 DINOv2 block; the DPT heads read all four), plus
+    a second chunk overlapping by 4 frames, so the GPU IRLS (:219-305) fits a
+    Sim(3) between full-size point maps (4 x 518^2 = 1.07 M points) and the
+    point maps / poses / depths are re-expressed through it.  HIP vs the
+    oracle's bf16-mixed emulation; the oracle's own fp32-vs-bf16 spread is
+    printed beside every error."""
+    import os
+    from aligned_vggt.backbone.aggregator import Aggregator
+    from aligned_vggt.models.pointAligned_wrapped_vggt import VGGT
+    from aligned_vggt.utils.synthetic import condition_pose_outputs_, synthetic_images, synthetic_init_
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    m = VGGT(enable_track=False)
+    m.aggregator = Aggregator(depth=4, dino_depth=1)
+    m.intermediate_layer_indices = [0, 1, 2, 3]
+    synthetic_init_(m, seed=11)
+    condition_pose_outputs_(m)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.cuda().eval()
+    S, ov, H, W = 8, 4, 518, 518
+    imgs = synthetic_images(1, 2 * S - ov, H, W, seed=1234)
+    chunks = O.generate_chunks(imgs.shape[1], S, ov)
+    assert [len(c) for c in chunks] == [8, 8]
+    agg_kw = {"keep": (0, 1, 2, 3), "depth": 4, "dino_depth": 1}
+    ref = ref32 = got = None
+    for ids in chunks:
+        x = imgs[:, ids]
+        with torch.no_grad():
+            ref = AO.point_aligned_forward(sd, x, ov, ref, bf16=True, agg_kwargs=agg_kw)
+            ref32 = AO.point_aligned_forward(sd, x, ov, ref32, bf16=False, agg_kwargs=agg_kw)
+        got = m(x.cuda(), ov, got)
+    torch.cuda.synchronize()
+    assert got["world_points"][-1].shape == (1, 8, 518, 518, 3)
+    assert got["depth"][-1].shape == (1, 8, 518, 518, 1)
+    worst = {}
+    for k in ("world_points", "world_points_conf", "depth", "depth_conf", "pose_enc"):
+        for c, (a, b, r32) in enumerate(zip(got[k], ref[k], ref32[k])):
+            assert torch.isfinite(a).all(), k
+            e_hip, e_ref = _rel(a, b), _rel(r32, b)
+            print(f"configs[0] chunk {c} {k}: hip vs bf16 oracle {e_hip:.3e}, oracle fp32 vs bf16 {e_ref:.3e}")
+            worst[k] = max(worst.get(k, 0.0), e_hip)
+            assert e_hip < max(1e-2, 1.5 * e_ref), (k, c, e_hip, e_ref)
+    print("configs[0] worst rel-L2:", worst)
