@@ -119,6 +119,85 @@ ALIGN_CASES = [("a1", "m8", 1, 3, 1, None), ("a2", "m8", 1, 3, 1, "a1"), ("a3", 
 FA_RUNS = [("ov2", 12, 5, 2, False), ("ov1", 8, 3, 1, False), ("gt", 8, 4, 2, True)]
 
 
+# training-gradient fixture (tests/golden/ref_train_grads.npz): two chunks of S
+# frames through the alignment head with memory, next overlap ov
+TRAIN_CASE = {"S": 4, "ov": 2}
+
+
+def train_inputs():
+    """(chunk 1, chunk 2) layer-23 tokens (1, S, P, 2048) of the gradient fixture."""
+    P = fix_tokens_per_frame()
+    S = TRAIN_CASE["S"]
+    return tuple(fixture_tensor(f"tr.tok{i}", (1, S, P, 2048), FIX_SEED) for i in (1, 2))
+
+
+def train_loss(o1, o2):
+    """The gradient fixture's loss: a fixed linear functional of both chunks'
+    (chunk_sim3, frame_se3, memory, new_overlap_tokens) outputs (on o1's device)."""
+    (cs1, fs1, m1, _), (cs2, fs2, m2, nov2) = o1, o2
+    S, ov = TRAIN_CASE["S"], TRAIN_CASE["ov"]
+    P = fix_tokens_per_frame()
+    dev = cs1.device
+    w = {k: fixture_tensor("tr.w" + k, shp, FIX_SEED).to(dev) for k, shp in
+         (("cs", (1, 1, 8)), ("fs", (1, S - 1, 7)), ("mem", (1, 8, 512)), ("ov", (1, ov + 1, P + 1, 1024)))}
+    return ((cs1.float() * w["cs"]).sum() + (fs1.float() * w["fs"]).sum() + (cs2.float() * w["cs"]).sum()
+            + 2 * (fs2.float() * w["fs"]).sum() + (m2.float() * w["mem"]).sum() + 1e-2 * (nov2.float() * w["ov"]).sum())
+
+
+GRAD_FULL_MAX = 8192  # parameters up to this size are stored whole
+GRAD_SAMPLES = 512
+
+
+def grad_indices(name: str, numel: int) -> np.ndarray:
+    """Fixed sampled flat indices of a large parameter's gradient."""
+    return np.sort(_rng(FIX_SEED, "gradidx:" + name).choice(numel, GRAD_SAMPLES, replace=False))
+
+
+def grad_sample(name: str, grad: torch.Tensor) -> Dict[str, np.ndarray]:
+    """What the fixture keeps of one parameter gradient: ``full`` (small ones)
+    or ``idx`` / ``val`` sampled entries plus the whole gradient's ``norm``."""
+    g = grad.detach().float().reshape(-1).cpu()
+    out = {"norm": np.array(float(g.double().norm()), dtype=np.float64)}  # fp64: an fp32 norm over 4 M entries is off by ~1e-4
+    if g.numel() <= GRAD_FULL_MAX:
+        out["full"] = g.numpy().copy()
+    else:
+        idx = grad_indices(name, g.numel())
+        out["val"] = g[torch.from_numpy(idx)].numpy().copy()
+    return out
+
+
+def _rel_l2(a, b) -> float:
+    a, b = torch.as_tensor(a).double(), torch.as_tensor(b).double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+ZERO_GRAD = 1e-5  # every non-degenerate gradient of the fixture has norm > 1e-3
+
+
+def grad_errors(g, prec: str, grads) -> Dict[str, float]:
+    """Per-parameter rel-L2 of ``grads`` (name -> full gradient) against the
+    fixture's stored entries (the whole gradient or its sampled indices) and
+    the relative error of the gradient norm."""
+    errs = {}
+    for key in g:
+        if not (key.startswith(prec + ".") and key.endswith(".norm")):
+            continue
+        name = key[len(prec) + 1:-len(".norm")]
+        gr = grads[name].detach().double().reshape(-1).cpu()
+        if float(g[key]) < ZERO_GRAD:
+            # mathematically zero: q / k / norm1 of the decoder's frame-cross blocks attend
+            # to ONE key (softmax == 1), so only rounding noise of order 1e-8 is stored
+            errs[name] = 0.0 if float(gr.norm()) < ZERO_GRAD else 1.0
+            continue
+        if f"{prec}.{name}.full" in g:
+            e = _rel_l2(gr, g[f"{prec}.{name}.full"])
+        else:
+            e = _rel_l2(gr[torch.from_numpy(grad_indices(name, gr.numel()))], g[f"{prec}.{name}.val"])
+        en = abs(float(gr.norm()) / max(float(g[key]), 1e-30) - 1.0)
+        errs[name] = max(e, en)
+    return errs
+
+
 def fix_tokens_per_frame() -> int:
     H, W = FIX_HW
     return 5 + (H // 14) * (W // 14)

@@ -476,9 +476,14 @@ def _fusion(sd: SD, p: str, x0: Tensor, x1: Optional[Tensor], size=None) -> Tens
 
 
 def dpt_head(sd: SD, p: str, tokens_list: List[Tensor], images: Tensor, patch_start_idx: int,
-             activation: str, conf_activation: str = "expp1", frames_chunk_size: int = 8) -> Tuple[Tensor, Tensor]:
+             activation: str, conf_activation: str = "expp1", frames_chunk_size: int = 8, pos_embed: bool = True,
+             stages: Optional[dict] = None) -> Tuple[Tensor, Tensor]:
     """DPTHead.forward (ext).  Frame chunking (frames_chunk_size) does not
-    change the arithmetic; all frames are processed at once here."""
+    change the arithmetic; all frames are processed at once here.
+    ``stages``: filled with the NCHW sub-stage outputs the third-party pin
+    (tests/golden/dpt_hf.npz) checks -- reassemble{i}, rn{i}, fused{j}
+    (j = 0 is refinenet4) and head_pre (before the activations)."""
+    st = stages if stages is not None else {}
     B, S, _, H, W = images.shape
     ps = 14
     ph, pw = H // ps, W // ps
@@ -490,27 +495,30 @@ def dpt_head(sd: SD, p: str, tokens_list: List[Tensor], images: Tensor, patch_st
         x = layer_norm(x, sd[p + "norm.weight"], sd[p + "norm.bias"], 1e-5)
         x = x.permute(0, 2, 1).reshape(B * S, x.shape[-1], ph, pw)
         x = _conv(sd, f"{p}projects.{li}.", x)
-        x = x + dpt_pos_embed(x.shape[1], ph, pw, W, H)
+        if pos_embed:
+            x = x + dpt_pos_embed(x.shape[1], ph, pw, W, H)
         if li == 0:
             x = F.conv_transpose2d(x, sd[p + "resize_layers.0.weight"], sd[p + "resize_layers.0.bias"], stride=4)
         elif li == 1:
             x = F.conv_transpose2d(x, sd[p + "resize_layers.1.weight"], sd[p + "resize_layers.1.bias"], stride=2)
         elif li == 3:
             x = _conv(sd, p + "resize_layers.3.", x, stride=2, padding=1)
+        st[f"reassemble{li}"] = x
         outs.append(x)
-    l1 = _conv(sd, p + "scratch.layer1_rn.", outs[0], padding=1)
-    l2 = _conv(sd, p + "scratch.layer2_rn.", outs[1], padding=1)
-    l3 = _conv(sd, p + "scratch.layer3_rn.", outs[2], padding=1)
-    l4 = _conv(sd, p + "scratch.layer4_rn.", outs[3], padding=1)
-    out = _fusion(sd, p + "scratch.refinenet4.", l4, None, size=l3.shape[2:])
-    out = _fusion(sd, p + "scratch.refinenet3.", out, l3, size=l2.shape[2:])
-    out = _fusion(sd, p + "scratch.refinenet2.", out, l2, size=l1.shape[2:])
-    out = _fusion(sd, p + "scratch.refinenet1.", out, l1)
+    ls = [_conv(sd, p + f"scratch.layer{i + 1}_rn.", outs[i], padding=1) for i in range(4)]
+    for i in range(4):
+        st[f"rn{i}"] = ls[i]
+    l1, l2, l3, l4 = ls
+    out = st["fused0"] = _fusion(sd, p + "scratch.refinenet4.", l4, None, size=l3.shape[2:])
+    out = st["fused1"] = _fusion(sd, p + "scratch.refinenet3.", out, l3, size=l2.shape[2:])
+    out = st["fused2"] = _fusion(sd, p + "scratch.refinenet2.", out, l2, size=l1.shape[2:])
+    out = st["fused3"] = _fusion(sd, p + "scratch.refinenet1.", out, l1)
     out = _conv(sd, p + "scratch.output_conv1.", out, padding=1)
     out = F.interpolate(out, size=(ph * ps, pw * ps), mode="bilinear", align_corners=True)
-    out = out + dpt_pos_embed(out.shape[1], out.shape[2], out.shape[3], W, H)
+    if pos_embed:
+        out = out + dpt_pos_embed(out.shape[1], out.shape[2], out.shape[3], W, H)
     out = F.relu(_conv(sd, p + "scratch.output_conv2.0.", out, padding=1))
-    out = _conv(sd, p + "scratch.output_conv2.2.", out)
+    out = st["head_pre"] = _conv(sd, p + "scratch.output_conv2.2.", out)
     fmap = out.permute(0, 2, 3, 1)
     xyz, conf = fmap[..., :-1], fmap[..., -1]
     if activation == "exp":

@@ -8,8 +8,9 @@ What it runs:
   * pure-torch/numpy functions pulled out of modules whose module-level
     ``vggt`` imports fail, by parsing the file with ``ast`` and executing only
     those ``def``s (no stand-in for the missing ``vggt`` package is written);
-  * ``transformers`` Dinov2WithRegistersModel (third-party, in-container) as an
-    independent pin of the DINOv2 stage.
+  * ``transformers`` Dinov2WithRegistersModel and the Depth-Anything DPT neck /
+    head (third-party, in-container) as independent pins of the DINOv2 stage
+    and of the DPT decoder arithmetic.
 
 Outputs are data only (inputs + expected outputs) in ``tests/golden/*.npz``.
 Usage:  python tests/golden/gen_golden.py [--ref /root/reference]
@@ -333,6 +334,80 @@ def gen_dinov2():
     save("dinov2_hf", **outs, **{"sd." + k: v for k, v in sd.items()})
 
 
+def gen_dpt_hf():
+    """Independent third-party pin of the DPT decoder arithmetic (ext VGGT
+    ``heads/dpt_head.py``, called at featureAligned_vggt.py:166 / :183): the
+    in-container ``transformers`` Depth-Anything neck + depth head, a DPT of
+    the same lineage -- reassemble (1x1 projection; ConvTranspose 4x / 2x,
+    identity, 3x3 stride-2 conv), the 3x3 ``layer*_rn`` convs, FeatureFusion
+    (pre-activation residual units, bilinear ``align_corners=True`` resize,
+    1x1 projection) and the output convs with the resize to full resolution.
+    Two VGGT deviations are configured, not patched: the residual units'
+    ReLU is in place (VGGT's ``nn.ReLU(inplace=True)``, so the skip adds
+    relu(x)), and the pre-activation head output is taken from ``conv3`` by a
+    forward hook.  Not covered here: DPT's positional embedding (VGGT-only),
+    the output activations.  Weights are stored under the VGGT DPTHead names."""
+    import torch.nn as nn
+    from transformers import DepthAnythingConfig
+    from transformers.models.depth_anything.modeling_depth_anything import (DepthAnythingDepthEstimationHead,
+                                                                            DepthAnythingNeck)
+    cin, oc, feat = 64, [32, 32, 64, 64], 64
+    cfg = DepthAnythingConfig(reassemble_hidden_size=cin, neck_hidden_sizes=oc, reassemble_factors=[4, 2, 1, 0.5],
+                              fusion_hidden_size=feat, head_hidden_size=32, head_in_index=-1, patch_size=14,
+                              depth_estimation_type="metric", max_depth=1)
+    torch.manual_seed(6)
+    neck, head = DepthAnythingNeck(cfg).eval(), DepthAnythingDepthEstimationHead(cfg).eval()
+    with torch.no_grad():
+        for mod in (neck, head):
+            for name, prm in mod.named_parameters():
+                fan_in = prm[0].numel() if prm.dim() > 1 else 1
+                prm.copy_(torch.randn_like(prm) * (0.5 / fan_in ** 0.5 if prm.dim() > 1 else 0.05))
+    for fl in neck.fusion_stage.layers:
+        for rl in (fl.residual_layer1, fl.residual_layer2):
+            rl.activation1 = nn.ReLU(inplace=True)
+    hf = {**{"neck." + k: v for k, v in neck.state_dict().items()}, **{"head." + k: v for k, v in head.state_dict().items()}}
+    sd = {"norm.weight": torch.ones(cin), "norm.bias": torch.zeros(cin)}
+    for i in range(4):
+        for t in ("weight", "bias"):
+            sd[f"projects.{i}.{t}"] = hf[f"neck.reassemble_stage.layers.{i}.projection.{t}"]
+            if i != 2:
+                sd[f"resize_layers.{i}.{t}"] = hf[f"neck.reassemble_stage.layers.{i}.resize.{t}"]
+        sd[f"scratch.layer{i + 1}_rn.weight"] = hf[f"neck.convs.{i}.weight"]
+    for j in range(4):  # the fusion stage runs the deepest level first: layer j = refinenet(4 - j)
+        d, s = f"neck.fusion_stage.layers.{j}.", f"scratch.refinenet{4 - j}."
+        for t in ("weight", "bias"):
+            sd[s + f"out_conv.{t}"] = hf[d + f"projection.{t}"]
+            for u in (1, 2):
+                for c in (1, 2):
+                    if j == 0 and u == 1:
+                        continue  # refinenet4 has no residual unit 1 (has_residual=False)
+                    sd[s + f"resConfUnit{u}.conv{c}.{t}"] = hf[d + f"residual_layer{u}.convolution{c}.{t}"]
+    g = torch.Generator().manual_seed(3)
+    for t in ("weight", "bias"):
+        sd[f"scratch.output_conv1.{t}"] = hf[f"head.conv1.{t}"]
+        sd[f"scratch.output_conv2.0.{t}"] = hf[f"head.conv2.{t}"]
+        extra = torch.randn((1,) + hf[f"head.conv3.{t}"].shape[1:], generator=g) * 0.05  # conf channel (unpinned)
+        sd[f"scratch.output_conv2.2.{t}"] = torch.cat([hf[f"head.conv3.{t}"], extra], 0)
+    F_, ph, pw = 2, 5, 7
+    tokens = torch.randn(F_, ph * pw, cin, generator=g)
+    x = F.layer_norm(tokens, (cin,), eps=1e-5)
+    hs = [torch.cat([torch.zeros(F_, 1, cin), x], 1) for _ in range(4)]  # index 0 = the (dropped) cls slot
+    cap = {}
+    hooks = [neck.reassemble_stage.layers[i].register_forward_hook(
+        lambda m, a, o, i=i: cap.__setitem__(f"reassemble{i}", o.clone())) for i in range(4)]
+    hooks += [neck.convs[i].register_forward_hook(
+        lambda m, a, o, i=i: cap.__setitem__(f"rn{i}", o.clone())) for i in range(4)]
+    hooks += [neck.fusion_stage.layers[j].register_forward_hook(
+        lambda m, a, o, j=j: cap.__setitem__(f"fused{j}", o.clone())) for j in range(4)]
+    hooks.append(head.conv3.register_forward_hook(lambda m, a, o: cap.__setitem__("head_pre", o.clone())))
+    with torch.no_grad():
+        feats = neck(hs, ph, pw)
+        out = head(feats, ph, pw)
+    for h in hooks:
+        h.remove()
+    save("dpt_hf", tokens=tokens, ph=ph, pw=pw, out_sigmoid=out, **cap, **{"sd." + k: v for k, v in sd.items()})
+
+
 # ----------------------------------------------------------------------------
 # the reference-authored alignment path, run on the test-only vggt shim
 # (SURVEY.md §4 item 2; weights / inputs from oracle.fixture_weights, not stored)
@@ -432,6 +507,51 @@ def gen_ref_alignment_head(ref):
     print("wrote ref_alignment_keys.json", {k: len(v) for k, v in keys.items()})
 
 
+def gen_ref_train_grads(ref):
+    """Training gradients of the reference's own AlignmentHead
+    (alignment_head.py:224-540 in train mode: torch.utils.checkpoint around every
+    block, the overlap tokens detached at :260, the memory recurrence keeping its
+    gradient at :482-484, GatedUpdate's detached gate input, gated_update.py:69)
+    over two chunks, for the fixed loss of oracle.fixture_weights.train_loss --
+    a linear functional of both chunks' Sim(3) / SE(3) outputs, chunk 2's memory
+    and new overlap tokens.  Frame dropout off (drop_prob_nonoverlap = 0; its mask
+    is tested separately).  fp32 and emulated bf16-mixed (forward AND backward
+    inside the emulation).
+    Stored per parameter: the full gradient when small, else the gradient at
+    fixed sampled indices plus its norm (oracle.fixture_weights.grad_sample)."""
+    shim, AH, _, _, _ = _ref_alignment_modules(ref)
+    import aligned_vggt.heads.alignment_head as ahmod  # the reference module
+    from oracle.fixture_weights import TRAIN_CASE, grad_sample, load_fixture_weights_, train_inputs, train_loss
+    S, ov = TRAIN_CASE["S"], TRAIN_CASE["ov"]
+    H, W = FIX_HW
+    out = {}
+    # torch.utils.checkpoint (alignment_head.py:361, :385, :498, :527) recomputes each
+    # block in backward outside the autocast emulation's TorchFunctionMode, so its
+    # recompute would not match the forward; a direct call has identical gradients
+    # (non-reentrant checkpointing only trades memory for recompute)
+    real_ckpt = ahmod.checkpoint
+    ahmod.checkpoint = lambda fn, *a, use_reentrant=None, **k: fn(*a, **k)
+    for prec in ("f32", "bf16"):
+        torch.manual_seed(0)
+        head = load_fixture_weights_(AH(in_dim=2048, patch_size=14, num_memory_tokens=8, temporal_attention=True),
+                                     FIX_SEED, prefix="alignment_head.").train()
+        head.drop_prob_nonoverlap = 0.0
+        tok1, tok2 = train_inputs()
+        with shim.bf16_mixed(prec == "bf16"):
+            o1 = head(tok1, (H, W), ov)
+            o2 = head(tok2, (H, W), ov, overlap_tokens=o1[3], memory_tokens=o1[2])
+            loss = train_loss(o1, o2)
+            loss.backward()
+        out[f"{prec}_loss"] = loss.detach().float()
+        for name, p in head.named_parameters():
+            if p.grad is None:
+                continue
+            for k, v in grad_sample(name, p.grad.float()).items():
+                out[f"{prec}.{name}.{k}"] = v
+    ahmod.checkpoint = real_ckpt
+    save("ref_train_grads", **out)
+
+
 def gen_ref_feature_aligned(ref):
     """FeatureAlignedVGGT.forward composition (featureAligned_vggt.py:73-225) over
     whole chunk sequences: the reference's alignment head + Sim(3)/SE(3)
@@ -493,7 +613,7 @@ def main():
     a = ap.parse_args()
     if a.only:
         for n in a.only.split(","):
-            globals()["gen_" + n](a.ref) if n != "dinov2" else gen_dinov2()
+            globals()["gen_" + n](a.ref) if n not in ("dinov2", "dpt_hf") else globals()["gen_" + n]()
         return
     gen_rope(a.ref)
     gen_gated_update(a.ref)
@@ -506,6 +626,7 @@ def main():
     gen_scale_alignment(a.ref)
     gen_small_fns(a.ref)
     gen_dinov2()
+    gen_dpt_hf()
     gen_ref_cross_attention(a.ref)
     gen_ref_alignment_head(a.ref)
     gen_ref_feature_aligned(a.ref)

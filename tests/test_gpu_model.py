@@ -317,3 +317,37 @@ def test_pipeline_grouped_encode_matches(models, H, W, N, w, ov):
             e = _rel(outs[g][k], outs[1][k])
             assert outs[g][k].shape == outs[1][k].shape, k
             assert e < 1e-5, (g, k, e)
+
+
+@pytest.mark.parametrize("conv,reorder,tol", [("bf16x3pre", True, 1e-4), ("bf16x3pre", False, 1e-4),
+                                              ("bf16x3", True, 1e-4), ("fp32", True, 2e-6)])
+def test_dpt_matches_transformers_depth_anything(golden, monkeypatch, conv, reorder, tol):
+    """HIP DPTHead (pos_embed off) vs the in-container transformers
+    Depth-Anything neck + head run with the same weights (tests/golden/dpt_hf.npz,
+    an independent third-party DPT: reassemble, layer*_rn, four fusion blocks with
+    the in-place-ReLU residual units, align_corners=True resizes at rectangular
+    sizes, output convs).  The depth channel's pre-activation is log(depth)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import numpy as np
+    from aligned_vggt.backbone import dpt_head as D
+    monkeypatch.setattr(D, "CONV_PRECISION", conv)
+    monkeypatch.setattr(D, "REORDER_OUT_CONV", reorder)
+    g = golden("dpt_hf")
+    sd = {k[3:]: torch.from_numpy(np.ascontiguousarray(v)) for k, v in g.items() if k.startswith("sd.")}
+    head = D.DPTHead(dim_in=64, features=64, out_channels=(32, 32, 64, 64), output_dim=2, activation="exp",
+                     pos_embed=False, intermediate_layer_idx=range(4))
+    head.load_state_dict(sd, strict=True)
+    head = head.cuda()
+    ph, pw = int(g["ph"]), int(g["pw"])
+    tok = torch.from_numpy(g["tokens"])
+    F_, hw, C = tok.shape
+    toks = torch.cat([torch.full((F_, 5, C), 7.0), tok], 1).reshape(1, F_, 5 + hw, C).cuda()
+    imgs = torch.zeros(1, F_, 3, ph * 14, pw * 14, device="cuda")
+    depth, conf = head([toks] * 4, images=imgs, patch_start_idx=5)
+    torch.cuda.synchronize()
+    pre = torch.log(depth[0, ..., 0]).cpu()
+    ref = torch.from_numpy(g["head_pre"][:, 0])
+    e = _rel(pre, ref)
+    print(f"DPT ({conv}, reorder={reorder}) vs transformers Depth-Anything: rel-L2 {e:.3e}")
+    assert pre.shape == ref.shape and e < tol, e

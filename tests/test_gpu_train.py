@@ -12,6 +12,7 @@ emulation: within 5e-2, or no further from the fp32 oracle than twice the
 oracle's own bf16-vs-fp32 spread (the same rule as the forward tests)."""
 import math
 
+import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
@@ -479,3 +480,38 @@ def test_graphed_training_step_matches_eager(N):
     assert losses[0] == losses[1], losses
     for (name, a), b in zip(heads[0].named_parameters(), heads[1].parameters()):
         assert torch.equal(a, b), (name, (a - b).abs().max().item())
+
+
+def test_alignment_head_gradients_vs_reference_fixture(N, golden):
+    """HIP training backward vs the parameter gradients of the reference's OWN
+    AlignmentHead in train mode (tests/golden/ref_train_grads.npz: two chunks,
+    memory recurrence, detached overlap tokens, the fixture's fixed loss; run on
+    the test-only vggt shim in fp32 and emulated bf16-mixed).  Every parameter
+    of the head is checked (whole small gradients, 512 sampled entries plus the
+    norm of large ones)."""
+    from aligned_vggt.heads.alignment_head import AlignmentHead
+    from oracle.fixture_weights import (FIX_HW, FIX_SEED, TRAIN_CASE, grad_errors, load_fixture_weights_,
+                                        train_inputs, train_loss)
+    g = golden("ref_train_grads")
+    torch.manual_seed(0)
+    head = AlignmentHead(in_dim=2048, patch_size=14, num_memory_tokens=8, temporal_attention=True)
+    head = load_fixture_weights_(head, FIX_SEED, prefix="alignment_head.").cuda().train()
+    head.drop_prob_nonoverlap = 0.0
+    tok1, tok2 = (t_.cuda() for t_ in train_inputs())
+    ov = TRAIN_CASE["ov"]
+    o1 = head(tok1, FIX_HW, ov)
+    o2 = head(tok2, FIX_HW, ov, overlap_tokens=o1[3], memory_tokens=o1[2])
+    loss = train_loss(o1, o2)
+    loss.backward()
+    torch.cuda.synchronize()
+    grads = {n: (p.grad if p.grad is not None else torch.zeros_like(p)) for n, p in head.named_parameters()}
+    e_bf, e_32 = grad_errors(g, "bf16", grads), grad_errors(g, "f32", grads)
+    assert len(e_bf) > 100 and set(e_bf) == set(e_32)
+    worst = sorted(e_bf, key=lambda k: -e_bf[k])[:6]
+    print("loss hip %.6f ref bf16 %.6f f32 %.6f" % (float(loss), float(g["bf16_loss"]), float(g["f32_loss"])))
+    print("HIP vs reference bf16-mixed gradients, worst:", [(k, round(e_bf[k], 5), round(e_32[k], 5)) for k in worst])
+    print("median rel error vs bf16 ref %.3e, vs fp32 ref %.3e" % (float(np.median(list(e_bf.values()))),
+                                                                  float(np.median(list(e_32.values())))))
+    assert abs(float(loss) / float(g["bf16_loss"]) - 1) < 1e-3
+    bad = {k: (e_bf[k], e_32[k]) for k in e_bf if not (e_bf[k] < 5e-2 or e_32[k] < 5e-2)}
+    assert not bad, bad

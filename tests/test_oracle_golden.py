@@ -66,6 +66,35 @@ def test_dinov2_stage_matches_transformers(golden):
         np.testing.assert_allclose(out.numpy(), g["patch_" + tag], rtol=1e-4, atol=1e-4)
 
 
+def _dpt_tokens(g, nspecial=5):
+    """The fixture's patch tokens as a (1, F, nspecial + h*w, C) aggregator layer
+    (special-token rows arbitrary: the DPT head reads from patch_start_idx)."""
+    tok = t(g["tokens"])
+    F_, hw, C = tok.shape
+    spec = torch.full((F_, nspecial, C), 7.0)
+    return torch.cat([spec, tok], 1).reshape(1, F_, nspecial + hw, C)
+
+
+def test_dpt_stages_match_transformers_depth_anything(golden):
+    """The oracle's DPT decoder vs the in-container transformers Depth-Anything
+    neck + head with the same weights (tests/golden/gen_golden.py gen_dpt_hf):
+    reassemble (incl. ConvTranspose 4x / 2x and the stride-2 conv), layer*_rn,
+    every fusion block (in-place-ReLU residual units, align_corners=True
+    resize, rectangular 3x4 -> 5x7 sizes) and the pre-activation head output."""
+    g = golden("dpt_hf")
+    sd = {k[3:]: t(v) for k, v in g.items() if k.startswith("sd.")}
+    ph, pw = int(g["ph"]), int(g["pw"])
+    toks = _dpt_tokens(g)
+    imgs = torch.zeros(1, toks.shape[1], 3, ph * 14, pw * 14)
+    st = {}
+    with torch.no_grad():
+        O.dpt_head(sd, "", [toks] * 4, imgs, 5, "exp", pos_embed=False, stages=st)
+    for k in [f"reassemble{i}" for i in range(4)] + [f"rn{i}" for i in range(4)] + [f"fused{j}" for j in range(4)]:
+        np.testing.assert_allclose(st[k].numpy(), g[k], rtol=1e-4, atol=2e-5, err_msg=k)
+    np.testing.assert_allclose(st["head_pre"][:, :1].numpy(), g["head_pre"], rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(torch.sigmoid(st["head_pre"][:, 0]).numpy(), g["out_sigmoid"], rtol=1e-5, atol=1e-6)
+
+
 def test_pose_roundtrip_known_answer():
     g = torch.Generator().manual_seed(0)
     q = torch.nn.functional.normalize(torch.randn(2, 5, 4, generator=g), dim=-1)
