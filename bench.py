@@ -60,12 +60,17 @@ def agg_flops(S=S_FRAMES, H=H_IMG, W=W_IMG, C=1024, depth=24, dino_depth=24):
 
 def cpu_baseline(threads: int):
     """Time the oracle (reference numerics, fp32, CPU) on a bounded sample of
-    the SAME workload at the full 16x518x518 chunk shape: the DINOv2 patch
-    embed + final LayerNorm, one DINOv2 block, one frame block, one global
-    block and the four kept-layer concats; the whole chunk = patch embed +
-    24 x each block kind + concats.  Threads: the GPU box's per-GPU CPU share
-    (16), not the whole host (os.cpu_count() reports every CPU of the
-    machine, shared with other jobs)."""
+    the SAME workload at the full 16x518x518 chunk shape (~20 s): the DINOv2
+    patch embed + final LayerNorm, one DINOv2 block, one frame block, one
+    global block and the four kept-layer concats, after a small warm-up pass;
+    the cheap blocks are timed 3 times (median), the global block (most of the
+    sample) once.  The whole chunk = patch embed + 24 x each block kind +
+    concats.  Threads: the GPU box's per-GPU CPU share (16), not the whole host
+    (os.cpu_count() reports every CPU of the machine, shared with other jobs).
+    The full-chunk measurements of scripts/cpu_baseline_full.py (1 warm-up +
+    3 timed whole chunks, median, at 16 and at os.cpu_count() threads;
+    BASELINE.md §3 rows C1 / C2) are attached from profiles/cpu_baseline_full.json."""
+    import statistics
     from oracle import vggt_oracle as O
     from aligned_vggt.backbone.aggregator import Aggregator
     from aligned_vggt.utils.synthetic import synthetic_images, synthetic_init_
@@ -79,25 +84,38 @@ def cpu_baseline(threads: int):
     x = torch.randn(S_FRAMES, P, 1024, generator=g)
     imgs = synthetic_images(1, S_FRAMES, H_IMG, W_IMG)[0]
     pos = O.position_grid(S_FRAMES, H_IMG // 14, W_IMG // 14, 5)
+
+    def timed(fn, n=1):
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return statistics.median(ts)
+
     with torch.no_grad():
         t0 = time.perf_counter()
-        O.dinov2(sd, "aggregator.patch_embed.", imgs, False, depth=0)
-        t1 = time.perf_counter()
-        O.block(sd, "aggregator.patch_embed.blocks.0.", x, 16, eps=1e-6)
-        t2 = time.perf_counter()
-        O.block(sd, "aggregator.frame_blocks.0.", x, 16, pos, "2d", True)
-        t3 = time.perf_counter()
-        O.block(sd, "aggregator.global_blocks.0.", x.view(1, S_FRAMES * P, 1024), 16, pos.view(1, -1, 2), "2d", True)
-        t4 = time.perf_counter()
-        for _ in range(4):
-            torch.cat([x, x], dim=-1)
-        t5 = time.perf_counter()
-    sec_chunk = (t1 - t0) + 24 * (t2 - t1) + 24 * (t3 - t2) + 24 * (t4 - t3) + (t5 - t4)
-    return {"value": 1.0 / sec_chunk, "unit": "chunks/s", "cores": threads, "kind": "port",
-            "host_cpu": _cpu_model(), "host_logical_cpus": os.cpu_count(),
-            "sample": f"oracle fp32 CPU (reference numerics) at 16x518x518: patch embed + final LN, 1 DINOv2 + "
-                      f"1 frame + 1 global block, 4 kept-layer concats ({t5 - t0:.1f} s measured); blocks scaled "
-                      f"x24 each to a full aggregator chunk ({sec_chunk:.1f} s/chunk)"}
+        O.block(sd, "aggregator.frame_blocks.0.", x[:2], 16, pos[:2], "2d", True)  # warm-up
+        warm = time.perf_counter() - t0
+        t_patch = timed(lambda: O.dinov2(sd, "aggregator.patch_embed.", imgs, False, depth=0))
+        t_dino = timed(lambda: O.block(sd, "aggregator.patch_embed.blocks.0.", x, 16, eps=1e-6), 3)
+        t_frame = timed(lambda: O.block(sd, "aggregator.frame_blocks.0.", x, 16, pos, "2d", True), 3)
+        t_glob = timed(lambda: O.block(sd, "aggregator.global_blocks.0.", x.view(1, S_FRAMES * P, 1024), 16,
+                                       pos.view(1, -1, 2), "2d", True))
+        t_cat = timed(lambda: [torch.cat([x, x], dim=-1) for _ in range(4)])
+    sec_chunk = t_patch + 24 * (t_dino + t_frame + t_glob) + t_cat
+    out = {"value": 1.0 / sec_chunk, "unit": "chunks/s", "cores": threads, "kind": "port",
+           "host_cpu": _cpu_model(), "host_logical_cpus": os.cpu_count(),
+           "sample": f"oracle fp32 CPU (reference numerics) at 16x518x518 after a {warm:.1f} s warm-up: patch embed "
+                     f"+ final LN {t_patch:.2f} s, DINOv2 block {t_dino:.2f} s and frame block {t_frame:.2f} s "
+                     f"(median of 3 each), global block {t_glob:.2f} s, 4 kept-layer concats; blocks scaled x24 "
+                     f"each to a full aggregator chunk ({sec_chunk:.1f} s/chunk)"}
+    try:
+        with open(os.path.join(ROOT, "profiles", "cpu_baseline_full.json")) as fh:
+            out["full_chunk_measured"] = json.load(fh)
+    except (OSError, ValueError):
+        pass
+    return out
 
 
 def _cpu_model() -> str:
@@ -133,7 +151,7 @@ def _launch(args) -> int:
 
 
 # BASELINE.json configs as presets: (workload, seq_frames, height, frames, overlap, memory tokens)
-CONFIGS = {1: ("aggregator", None, 518, 16, 4, 8), 2: ("sequence", 64, 518, 16, 4, 8),
+CONFIGS = {0: ("point", None, 518, 8, 0, 0), 1: ("aggregator", None, 518, 16, 4, 8), 2: ("sequence", 64, 518, 16, 4, 8),
            3: ("sequence", 512, 154, 16, 4, 0), 4: ("sequence", 512, 154, 16, 4, 8)}
 
 
@@ -173,8 +191,10 @@ def main():
                     help="BASELINE.json configs[i] preset (sets workload / frames / size / memory)")
     ap.add_argument("--memory-tokens", type=int, default=8, help="alignment-head memory tokens (0: no memory)")
     ap.add_argument("--workload", default="aggregator",
-                    choices=["aggregator", "chunk", "sequence", "train", "selftest"],
-                    help="aggregator: BASELINE configs[1] headline (default); chunk: full FeatureAlignedVGGT "
+                    choices=["aggregator", "point", "chunk", "sequence", "train", "selftest"],
+                    help="aggregator: BASELINE configs[1] headline (default); point: configs[0], one 8-frame "
+                         "518^2 chunk through the point-aligned VGGT (aggregator + point / depth / camera heads); "
+                         "chunk: full FeatureAlignedVGGT "
                          "per-chunk forward (encoder + alignment head + camera/depth heads); sequence: configs[2..4] "
                          "chunk pipeline over --seq-frames frames (RCCL baton ring at N>1); train: one alignment-head "
                          "training step (two chunks with memory recurrence, forward + backward + AdamW) on resident "
@@ -186,6 +206,8 @@ def main():
     ap.add_argument("--frames", type=int, default=S_FRAMES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--cpu-runs", type=int, default=1,
+                    help="point workload: timed full-chunk CPU runs after the warm-up (BASELINE.md §3 asks for 3)")
     args = ap.parse_args()
     if args.config is not None:
         args.workload, seq, args.height, args.frames, args.overlap, args.memory_tokens = CONFIGS[args.config]
@@ -215,6 +237,8 @@ def main():
 
     if args.workload == "train":
         return bench_train(args, world, rank, dev)
+    if args.workload == "point":
+        return bench_point(args, world, rank, dev)
     if args.workload != "aggregator":
         return bench_full(args, world, rank, dev)
 
@@ -433,6 +457,107 @@ def _recurrence_probe(pipe, step, n_chunks, t1_ms, world):
         out["T1_over_8_ms"] = round(t1_ms / 8, 1)
         out["bound_frac_of_T1_over_8"] = round(n_chunks * t_load / (t1_ms / 8), 3)
     return out
+
+
+def bench_point(args, world, rank, dev):
+    """BASELINE configs[0]: one 8-frame 518 x 518 synthetic chunk through the
+    point-aligned VGGT (pointAligned_wrapped_vggt.py:34-157: aggregator,
+    point / depth DPT heads, camera head; a first chunk, so the Sim(3) is the
+    identity, :96-98), random-init weights, per rank per step (replicas)."""
+    import torch.distributed as dist
+    from aligned_vggt import _native
+    from aligned_vggt.models.pointAligned_wrapped_vggt import VGGT
+    from aligned_vggt.utils.synthetic import condition_pose_outputs_, synthetic_images, synthetic_init_
+    S, H, W = args.frames, args.height, W_IMG
+    model = VGGT(enable_track=False)
+    synthetic_init_(model, seed=0)
+    condition_pose_outputs_(model)
+    cpu_sd = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu_sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    model = model.to(dev).eval()
+    imgs = synthetic_images(1, S, H, W, seed=1234 + rank, device=dev)
+    timer = EventTimer({"global_attn"})
+    _native.EVENT_HOOK = timer
+
+    def step():
+        return model(imgs, 0, None)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timer.active = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    timer.active = False
+    attn_ms = timer.mean_ms()
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+        dist.destroy_process_group()
+    if rank != 0:
+        return
+    fl = agg_flops(S=S, H=H, W=W)
+    value = args.steps * world / dt
+    attn_tf = fl["global_attn_launch"] / (attn_ms * 1e-3) / 1e12 if attn_ms else None
+    line = {
+        "metric": "chunks/sec (%d-frame %dx%d) point-aligned VGGT chunk" % (S, H, W),
+        "value": round(value, 4), "unit": "chunks/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (uniform [0,1) frames, random-init weights)",
+        "config": {"workload": "point-aligned VGGT (aggregator bf16 + point / depth DPT heads + camera head fp32), "
+                               "1 chunk of %d frames %dx%d" % (S, H, W), "baseline_config": 0, "frames": S,
+                   "parallelism": "replicas x%d" % world},
+        "tflops_per_gpu_aggregator": round(fl["total"] * value / world / 1e12, 1),
+        "roofline": {"bound": "mfma", "kernel": "attn_fwd_kernel<64> (global attention, 1x16 heads x %d^2 x 64)"
+                     % (S * (5 + (H // 14) * (W // 14))),
+                     "achieved": round(attn_tf, 1) if attn_tf else None, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(attn_tf / PEAK_BF16_TFLOPS, 4) if attn_tf else None,
+                     "avg_launch_ms": round(attn_ms, 4) if attn_ms else None,
+                     "flops_per_launch": fl["global_attn_launch"], "traffic": None},
+    }
+    if cpu_sd is not None:
+        line["cpu_baseline"] = cpu_baseline_point(cpu_sd, S, H, W, args.cpu_threads, args.cpu_runs)
+    print(json.dumps(line), flush=True)
+
+
+def cpu_baseline_point(sd, S, H, W, threads: int, runs: int):
+    """the oracle's fp32 point-aligned VGGT (reference
+    numerics) on one full 8-frame 518^2 chunk on the host cores: one warm-up
+    pass at reduced depth (page-in, thread pool), then ``runs`` timed full
+    chunks, median."""
+    import statistics
+    from oracle import alignment_oracle as AO
+    from aligned_vggt.utils.synthetic import synthetic_images
+    torch.set_num_threads(threads)
+    imgs = synthetic_images(1, S, H, W, seed=1234)
+    ts = []
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        AO.point_aligned_forward(sd, imgs[:, :2], 0, None,
+                                 agg_kwargs={"keep": (0, 1, 2, 3), "depth": 4, "dino_depth": 1})
+        warm = time.perf_counter() - t0
+        for _ in range(max(1, runs)):
+            t0 = time.perf_counter()
+            AO.point_aligned_forward(sd, imgs, 0, None)
+            ts.append(time.perf_counter() - t0)
+    med = statistics.median(ts)
+    return {"value": 1.0 / med, "unit": "chunks/s", "cores": threads, "kind": "port", "host_cpu": _cpu_model(),
+            "host_logical_cpus": os.cpu_count(),
+            "sample": f"oracle fp32 CPU point-aligned VGGT, one full {S}-frame {H}x{W} chunk (aggregator 24+24+24 "
+                      f"blocks, point + depth DPT heads, camera head): warm-up {warm:.1f} s (2 frames, reduced depth), "
+                      f"{len(ts)} timed run(s) {[round(x, 1) for x in ts]} s, median {med:.1f} s/chunk"}
 
 
 def bench_train(args, world, rank, dev):

@@ -826,7 +826,9 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
   // in the model (r6d: global 1.87 vs 1.84 ms per launch, step 100.8 vs 100.5
   // ms, configs[3] 1329 vs 1299 ms)
   // VGGT_ATTN16=2: the 16x16 form only for the 4-wave (nq < 4096: frame / DINOv2) launches
-  const bool use16 = D == 64 && nw != 2 &&
+  // (never with an lse: the training recompute, vggt_attention_fwd_lse, always
+  // takes the exact-score 32x32 form whose lse the backward recomputes bit for bit)
+  const bool use16 = a.lse == nullptr && D == 64 && nw != 2 &&
                      (g_vggt_attn_variant == 161 ||
                       (g_vggt_attn_variant == 33 && (g_vggt_attn16 == 1 || (g_vggt_attn16 == 2 && nw == 4))));
   if (use16) {

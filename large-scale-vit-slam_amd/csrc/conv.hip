@@ -612,14 +612,8 @@ __global__ __launch_bounds__(NT, 2) void conv_pre_kernel(ConvArgs a, const bf16_
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-#ifdef VGGT_CONV_STAGE_LATE
-    // (diagnostic variant) this step's fragment reads first, the next step's DMA issue while they land
-    reads(cur);
-    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
-#else
     if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
     reads(cur);
-#endif
     mfmas();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

@@ -1289,11 +1289,6 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
       // Bit 11 (with bit 9): half 0 issues every W piece of K-tile kt+1 (its own and half 1's rows,
       // the latter 128 rows on through the scalar offset) and half 1 only its A pieces, which it then
       // waits for at the end of MATH(kt) like half 0 -- no READ segment waits on DMA at all.
-#ifdef VGGT_KO_DMA
-      constexpr bool ko_dma = true;  // diagnostic build only (wrong results): no in-loop DMA
-#else
-      constexpr bool ko_dma = false;
-#endif
       // the default placement (bit 11) as its own copy of the loop, with no runtime
       // placement branches in it
       auto fk_loop = [&](auto wallc, auto rfc) {
@@ -1312,7 +1307,7 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
               read_frags(buf, 0);
               read_frags2(buf);
             }
-            if (pf && !ko_dma) {
+            if (pf) {
               if (wm == 0) {
                 stage_w(buf ^ 1, kt + 1);
                 stage_w2(buf ^ 1, kt + 1);
@@ -1324,7 +1319,7 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
               read_frags2(buf);
             }
           } else {
-            if (pf && !mh1 && !ko_dma) {
+            if (pf && !mh1) {
               stage_w(buf ^ 1, kt + 1);
               stage_a(buf ^ 1, kt + 1);
             }
@@ -1356,7 +1351,7 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
         for (int kt = 0; kt < nk; ++kt) {
           const int buf = (b0 + kt) & 1;
           const bool pf = kt >= 1 && kt + 1 < nk;
-          if (pf && !ko_dma) {
+          if (pf) {
             if (wm == 0) stage_w(buf ^ 1, kt + 1);
             stage_a(buf ^ 1, kt + 1);
           }
@@ -1369,7 +1364,7 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
           __builtin_amdgcn_sched_barrier(0);
           math2();
           __builtin_amdgcn_sched_barrier(0);
-          const bool w1 = wm == 1 && kt + 2 < nk && !ko_dma;
+          const bool w1 = wm == 1 && kt + 2 < nk;
           if (w1) stage_w(buf, kt + 2);
           if (wm == 0) {
             if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NST) : "memory");
@@ -1456,17 +1451,6 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
           rx[ni][mi] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, (ml * (int)ep.ldo + nl) * 4, 0, 0));
         }
     }
-#ifdef VGGT_EPI_BIAS_EARLY
-    // the plain / GELU epilogue's bias values from LDS before the next tile's DMA is issued
-    f32x4 bvs[C::NI];
-    if constexpr (EPI != VGGT_EPI_F32 && EPI != VGGT_EPI_RESID_F32) {  // (the fused qkv's v block too)
-#pragma unroll
-      for (int ni = 0; ni < C::NI; ++ni) bvs[ni] = *(const f32x4*)(bias_s + n0 + wn * C::WN + ni * 16 + 4 * (lane >> 4));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int ni = 0; ni < C::NI; ++ni) asm volatile("" : "+v"(bvs[ni]));
-    }
-#endif
     // the next tile's K-tiles 0 and 1, in flight during this epilogue
     const int next = tile + gridDim.x;
     const bool more = next < ntiles;
@@ -1598,19 +1582,6 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
           __builtin_amdgcn_raw_buffer_store_b128(pk, ro, (ml * (int)ep.ldo + hb + np * 16 + ncol) * 2, 0, 0);
         }
       }
-#ifdef VGGT_KO_EPI
-    } else if (EPI == VGGT_EPI_BF16 || EPI == VGGT_EPI_GELU_BF16) {
-      // diagnostic build only (wrong results): the same NST 16-B stores of raw accumulator bits, no epilogue math
-      const int ncol = (rg & 1) * 16 + (rg >> 1) * 8;
-#pragma unroll
-      for (int np = 0; np < C::NI; np += 2)
-#pragma unroll
-        for (int mi = 0; mi < C::MI; ++mi) {
-          const int ml = wm * C::HM + mi * 16 + (lane & 15);
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[np][mi]), ro,
-                                                 (ml * (int)ep.ldo + n0 + wn * C::WN + np * 16 + ncol) * 2, 0, 0);
-        }
-#endif
     } else {
       // after the swap, row group rg holds fragment ni + (rg & 1), features 8 * (rg >> 1) ..
       const int ncol = (rg & 1) * 16 + (rg >> 1) * 8;
@@ -1620,12 +1591,8 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
       (void)rpre;
 #pragma unroll
       for (int np = 0; np < C::NI; np += 2) {
-#ifdef VGGT_EPI_BIAS_EARLY
-        const f32x4 bv0 = bvs[np], bv1 = bvs[np + 1];
-#else
         const f32x4 bv0 = *(const f32x4*)(bias_s + n0 + wn * C::WN + np * 16 + 4 * rg);
         const f32x4 bv1 = *(const f32x4*)(bias_s + n0 + wn * C::WN + (np + 1) * 16 + 4 * rg);
-#endif
         const int nl = n0 + wn * C::WN + np * 16 + ncol;
 #pragma unroll
         for (int mi = 0; mi < C::MI; ++mi) {
@@ -1715,11 +1682,7 @@ inline int ppp_pick_bm(int epi, int M, int N) {
   const int cus = cu_count();
   const long r256 = ((long)((M + 255) / 256) * (N / 256) + cus - 1) / cus;
   const long r192 = ((long)((M + 191) / 192) * (N / 256) + cus - 1) / cus;
-#ifdef VGGT_BM_RULE_LE
-  return r192 * 192 * 10 <= r256 * 256 * 9 ? 192 : 256;
-#else
   return r192 * 192 * 10 < r256 * 256 * 9 ? 192 : 256;
-#endif
 }
 
 template <int EPI, int BMT, bool FK>

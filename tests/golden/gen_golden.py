@@ -351,7 +351,7 @@ def gen_dpt_hf():
     from transformers import DepthAnythingConfig
     from transformers.models.depth_anything.modeling_depth_anything import (DepthAnythingDepthEstimationHead,
                                                                             DepthAnythingNeck)
-    cin, oc, feat = 64, [32, 32, 64, 64], 64
+    cin, oc, feat = 256, [32, 32, 64, 64], 64  # cin: the HIP row LayerNorm takes C % 256 == 0
     cfg = DepthAnythingConfig(reassemble_hidden_size=cin, neck_hidden_sizes=oc, reassemble_factors=[4, 2, 1, 0.5],
                               fusion_hidden_size=feat, head_hidden_size=32, head_in_index=-1, patch_size=14,
                               depth_estimation_type="metric", max_depth=1)

@@ -42,7 +42,9 @@ def test_aggregator_small_depth(cuda):
         assert torch.isfinite(o).all()
         e, e32 = _rel(o, r), _rel(r32, r)
         print("aggregator small depth: hip vs bf16 oracle %.3e, oracle fp32 vs bf16 %.3e" % (e, e32))
-        assert e < 2e-2, (e, e32)
+        # no further from the bf16 emulation than the reference numerics' own
+        # bf16-vs-fp32 spread (measured on MI355X: 3.1e-3 vs 4.7e-3)
+        assert e < 1.25 * e32, (e, e32)
 
 
 def test_aggregator_full_depth_two_frames(cuda):
@@ -52,14 +54,14 @@ def test_aggregator_full_depth_two_frames(cuda):
         assert torch.isfinite(o).all()
         e, e32 = _rel(o, r), _rel(r32, r)
         print("aggregator full depth: hip vs bf16 oracle %.3e, oracle fp32 vs bf16 %.3e" % (e, e32))
-        assert e < 3e-2, (e, e32)
+        assert e < 1.25 * e32, (e, e32)  # measured 6.2e-3 vs 7.1e-3
 
 
 def test_aggregator_batch2(cuda):
     outs, ref, ref32 = _run(cuda, depth=2, dino_depth=1, B=2, S=2, H=42, W=56, keep=(1,))
     e, e32 = _rel(outs[0], ref[0]), _rel(ref32[0], ref[0])
     print("aggregator batch 2: hip vs bf16 oracle %.3e, oracle fp32 vs bf16 %.3e" % (e, e32))
-    assert e < 2e-2, (e, e32)
+    assert e < 1.25 * e32, (e, e32)  # measured 2.1e-3 vs 4.0e-3
 
 
 def test_aggregator_fused_add_ln_matches_epilogue_path(cuda, monkeypatch):
@@ -98,4 +100,4 @@ def test_aggregator_fused_add_ln_matches_epilogue_path(cuda, monkeypatch):
     for u, v in zip(a, b):
         e = _rel(u, v)
         print("fused add+LN vs RMW epilogue rel-L2 %.3e" % e)
-        assert e < 2e-3, e
+        assert e < 1e-6, e  # the same fp32 operations in the same order: measured bitwise equal

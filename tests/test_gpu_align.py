@@ -134,6 +134,15 @@ def test_point_aligned_two_chunks_vs_oracle(point_model):
             assert e_hip < max(3e-2, 1.5 * e_ref), (k, e_hip, e_ref)
 
 
+# configs[0] bars: ~2-3x the MI355X measurement (round 4: points 3.0e-4, confidences 3e-6,
+# depth 5.7e-4 on the aligned chunk -- the Sim(3) scale from the IRLS, whose reductions run
+# in fp64 on the GPU but in fp32 over 1.07 M points in the reference / oracle -- and 3.7e-6
+# on the first); the camera-head pose encodings of the random-init model amplify bf16 token
+# rounding (measured 2.0e-2 vs the oracle's own bf16-vs-fp32 spread of 1.7-1.9e-2) and keep
+# the spread-relative bar
+CONFIG0_BARS = {"world_points": 1e-3, "world_points_conf": 1e-4, "depth": 2e-3, "depth_conf": 1e-4}
+
+
 def test_point_aligned_config0_full_size_two_chunks(N):
     """BASELINE configs[0] at its size: 8-frame 518 x 518 chunks through the
     point-aligned VGGT (pointAligned_wrapped_vggt.py:34-157), reduced depth
@@ -177,5 +186,5 @@ def test_point_aligned_config0_full_size_two_chunks(N):
             e_hip, e_ref = _rel(a, b), _rel(r32, b)
             print(f"configs[0] chunk {c} {k}: hip vs bf16 oracle {e_hip:.3e}, oracle fp32 vs bf16 {e_ref:.3e}")
             worst[k] = max(worst.get(k, 0.0), e_hip)
-            assert e_hip < max(1e-2, 1.5 * e_ref), (k, c, e_hip, e_ref)
+            assert e_hip < CONFIG0_BARS.get(k, max(3e-2, 1.5 * e_ref)), (k, c, e_hip, e_ref)
     print("configs[0] worst rel-L2:", worst)

@@ -53,7 +53,7 @@ def test_aggregator_headline_chunk_reduced_depth(cuda):
         assert torch.isfinite(o).all()
         e = _rel(o, r)
         print("headline chunk layer rel-L2 vs bf16 oracle", e)
-        assert e < 2e-2, e
+        assert e < 4e-3, e  # measured 1.7e-3 (round 3); 2x that, rounded up
 
 
 def test_vkitti_sequence_with_tail_reduced_depth(cuda, monkeypatch):
