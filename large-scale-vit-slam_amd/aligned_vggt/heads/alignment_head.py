@@ -269,6 +269,18 @@ class AlignmentHead(nn.Module):
 
     def _forward_infer(self, tokens: torch.Tensor, image_size: Tuple[int, int], next_num_overlap: int,
                        overlap_tokens: torch.Tensor = None, memory_tokens: torch.Tensor = None):
+        x = self.prepare_infer(tokens, image_size)
+        B, S, P, _ = tokens.shape
+        return self.forward_prepared(x, (B, S, P), image_size, next_num_overlap, overlap_tokens, memory_tokens)
+
+    @torch.no_grad()
+    def prepare_infer(self, tokens: torch.Tensor, image_size: Tuple[int, int]) -> torch.Tensor:
+        """The context-free prefix of the inference forward (alignment_head.py:242-270
+        and the first frame block, :347-366): project_in, token_norm, the
+        per-frame alignment tokens and frame block 0 depend only on this
+        chunk's aggregator tokens, not on the previous chunk -- the multi-GPU
+        pipeline runs them with the encode, off the alignment recurrence.
+        Returns the fp32 residual rows [round_up(B*S*(P+1), 256), C]."""
         if tokens.device.type != "cuda":
             raise RuntimeError("AlignmentHead: the MI355X hot path runs on HIP devices only (no CPU fallback)")
         if not self.temporal_attention:
@@ -295,7 +307,25 @@ class AlignmentHead(nn.Module):
                             P1, 1)
         al = self.per_frame_alignment_token[0].detach().float().contiguous()  # (2, 1, C)
         N.special_tokens(x, B * S, S, P1, al)
+        r2 = self._rope2d(H_img // self.patch_size, W_img // self.patch_size, dev)
+        self.frame_blocks[0].forward_rows(x, M, (B * S, P1, P1), r2, ws, tag="align_frame_attn")
+        return x
 
+    @torch.no_grad()
+    def forward_prepared(self, x: torch.Tensor, bsp: Tuple[int, int, int], image_size: Tuple[int, int],
+                         next_num_overlap: int, overlap_tokens: torch.Tensor = None,
+                         memory_tokens: torch.Tensor = None):
+        """The recurrent part of the inference forward (alignment_head.py:270-345
+        from the first temporal block on), on the rows ``prepare_infer`` made
+        (updated in place).  ``bsp`` = (B, S, P) of the aggregator tokens."""
+        B, S, P = bsp
+        H_img, W_img = image_size
+        C = self.embed_dim
+        dev = x.device
+        ws = Workspace.get(dev)
+        P1 = P + 1
+        M = B * S * P1
+        assert x.shape[0] >= M and x.shape[1] == C and x.dtype == torch.float32
         first_chunk = overlap_tokens is None
         if not first_chunk:
             assert overlap_tokens.shape[0] == B and overlap_tokens.shape[2] == 1 + P and \
@@ -320,7 +350,8 @@ class AlignmentHead(nn.Module):
         ph, pw = H_img // self.patch_size, W_img // self.patch_size
         r2 = self._rope2d(ph, pw, dev)
         for i in range(self.aa_block_num):
-            self.frame_blocks[i].forward_rows(x, M, (B * S, P1, P1), r2, ws, tag="align_frame_attn")
+            if i > 0:  # frame block 0 ran in prepare_infer
+                self.frame_blocks[i].forward_rows(x, M, (B * S, P1, P1), r2, ws, tag="align_frame_attn")
             self.temporal_blocks[i].forward_rows_bf16(x, M, y, My, B * P1, S, nk, rq, rk, ws)
 
         tok4 = x[:M].view(B, S, P1, C)

@@ -23,6 +23,7 @@ from ..backbone.camera_head import CameraHead
 from ..backbone.dpt_head import DPTHead
 from ..backbone.track_head import TrackHead
 from ..heads.alignment_head import AlignmentHead
+from ..runtime import round_up
 from ..utils.data import extri_to_pose_encoding, pose_encoding_to_extri
 from ..utils.geometry import averagePoseEncodings, closed_form_inverse_se3
 from ..utils.pose_enc import extri_intri_to_pose_encoding, pose_encoding_to_extri_intri
@@ -34,6 +35,14 @@ from ..utils.pose_enc import extri_intri_to_pose_encoding, pose_encoding_to_extr
 # (~300 small launches per chunk, profiles/r4w).  Training always takes the
 # differentiable torch form.
 _POSE_MODE = os.environ.get("VGGT_POSE", "hip")
+# no-grad inference: the recurrent part of align_chunk (alignment head from its first
+# temporal block on, decoder, GatedUpdate, pose composition: ~300 launches, most of
+# them microseconds long) replays as ONE HIP graph per shape (_AlignGraph), and the
+# head's context-free prefix (project_in, token_norm, frame block 0) runs in
+# encode_chunk, off the recurrence.  VGGT_ALIGN_GRAPH=0: eager launches;
+# VGGT_ALIGN_PREFIX=0: the whole head in align_chunk.
+_ALIGN_GRAPH = os.environ.get("VGGT_ALIGN_GRAPH", "1") != "0"
+_ALIGN_PREFIX = os.environ.get("VGGT_ALIGN_PREFIX", "1") != "0"
 
 try:  # optional, as in the reference (featureAligned_vggt.py:3); only used for from_pretrained
     from huggingface_hub import PyTorchModelHubMixin
@@ -111,6 +120,12 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
             enc["depth"], enc["depth_conf"] = self.depth_head(toks, images=images, patch_start_idx=patch_start_idx)
         if self.point_head is not None:
             enc["points"], enc["points_conf"] = self.point_head(toks, images=images, patch_start_idx=patch_start_idx)
+        if _ALIGN_PREFIX and not self.alignment_head.training and images.is_cuda:
+            # the alignment head's context-free prefix, as (B, S*(P+1), C) rows so a
+            # grouped encode's result splits per chunk along dim 0
+            P1 = toks[-1].shape[2] + 1
+            x = self.alignment_head.prepare_infer(toks[-1], (H, W))
+            enc["ah_prep"] = x[:B * S * P1].view(B, S * P1, x.shape[1])
         return enc
 
     def align_chunk(self, enc: dict, num_overlap: int, context: dict = None, gt_poses: torch.Tensor = None) -> dict:
@@ -129,15 +144,33 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
             if self.enable_memory:
                 ctx_memory = context["memory_tokens"][-1]
         overlap = num_overlap if S > num_overlap else S - 1
-        chunk_sim3_enc, frame_se3_enc, memory_tokens, overlap_tokens = self.alignment_head(
-            toks[-1], (H, W), overlap, overlap_tokens=ctx_overlap, memory_tokens=ctx_memory)
-
         dev = images.device
-        chunk_scale = chunk_sim3_enc[..., -1]  # on the device: depth / point scaling
         mode = "torch" if train or dev.type != "cuda" else _POSE_MODE
+        prep = enc.get("ah_prep") if not train else None
+        pre = None  # (aligned_pose_enc, point_transform) when composed with the head
+        if prep is not None:
+            ctx_pe = context["pose_enc"][-1] if context is not None else None
+            use_pose = self.camera_head is not None and mode == "hip" and (context is None or gt_poses is None)
+            core_in = (prep, (B, S, toks[-1].shape[2]), (H, W), overlap, ctx_overlap, ctx_memory,
+                       enc["cam_pose_enc"] if use_pose else None, ctx_pe if use_pose else None,
+                       self.point_head is not None)
+            if _ALIGN_GRAPH:
+                outs = self._align_graph(core_in)
+            else:
+                outs = _align_core(self.alignment_head, *core_in)
+            chunk_sim3_enc, frame_se3_enc, memory_tokens, overlap_tokens, pe, pt = outs
+            if use_pose:
+                pre = (pe, pt)
+        else:
+            chunk_sim3_enc, frame_se3_enc, memory_tokens, overlap_tokens = self.alignment_head(
+                toks[-1], (H, W), overlap, overlap_tokens=ctx_overlap, memory_tokens=ctx_memory)
+
+        chunk_scale = chunk_sim3_enc[..., -1]  # on the device: depth / point scaling
         point_transform = None
         if self.camera_head is not None:
-            if mode == "hip":
+            if pre is not None:
+                aligned_pose_enc, point_transform = pre
+            elif mode == "hip":
                 ctx_pe = context["pose_enc"][-1] if context is not None else None
                 gt0 = gt_poses[:, 0] if (context is not None and gt_poses is not None) else None
                 aligned_pose_enc, point_transform = N.pose_compose(
@@ -208,6 +241,20 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
                 predictions["images"] = context["images"]
         return predictions
 
+    def _align_graph(self, core_in):
+        """Replay the recurrent part of align_chunk from a HIP graph captured
+        for this shape (and these parameter values)."""
+        prep, bsp, hw, overlap, ctx_ov, ctx_mem, cam, ctx_pe, want_pt = core_in
+        head = self.alignment_head
+        sig = tuple((p.data_ptr(), p._version) for p in head.parameters())
+        shp = lambda t: None if t is None else tuple(t.shape)  # noqa: E731
+        key = (bsp, tuple(hw), overlap, shp(ctx_ov), shp(ctx_mem), shp(cam), shp(ctx_pe), want_pt, str(prep.device))
+        graphs = self.__dict__.setdefault("_mi355x_align_graphs", {})
+        g = graphs.get(key)
+        if g is None or g.sig != sig:
+            g = graphs[key] = _AlignGraph(head, core_in, sig)
+        return g(core_in)
+
     def _compose_torch(self, enc, chunk_sim3_enc, frame_se3_enc, context, gt_poses, overlap, images, adev):
         """featureAligned_vggt.py:96-143 (+ the point transform of :187-196) as torch
         ops on ``adev`` (training: differentiable on the device).  Returns the
@@ -249,6 +296,69 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
         else:
             pt = point_identity_alignment.view(B, 1, 4, 4)
         return aligned_pose_enc.to(dev), pt.to(dev)
+
+
+def _align_core(head, prep, bsp, hw, overlap, ctx_ov, ctx_mem, cam, ctx_pe, want_pt, x=None):
+    """The recurrent part of the no-grad align_chunk: alignment head from its
+    first temporal block on (on a private padded copy of the prefix rows) and,
+    given the camera-head encoding, the pose composition
+    (featureAligned_vggt.py:94-143, vggt_pose_compose)."""
+    B, S, P = bsp
+    M = B * S * (P + 1)
+    if x is None:
+        x = torch.empty(round_up(M, 256), prep.shape[-1], device=prep.device, dtype=torch.float32)
+    x[:M].copy_(prep.reshape(M, -1))
+    cs, fs, mem, nov = head.forward_prepared(x, bsp, hw, overlap, ctx_ov, ctx_mem)
+    pe = pt = None
+    if cam is not None:
+        pe, pt = N.pose_compose(cs, fs, cam, ctx_pe, None, overlap, hw, want_point_transform=want_pt)
+    return cs, fs, mem, nov, pe, pt
+
+
+class _AlignGraph:
+    """One HIP graph of _align_core for one input shape.  Inputs are copied
+    into static buffers, the graph replays on the current stream, outputs are
+    cloned out (the next replay overwrites them).  Captured on a stream of its
+    own: the per-(device, stream) workspaces and split-K scratch the kernels
+    read are then that stream's alone and never grow (and move) after capture.
+    Parameter values are baked in through the cached operand packs -- the
+    owner re-captures when any parameter's (storage, version) changes."""
+
+    def __init__(self, head, core_in, sig):
+        prep, bsp, hw, overlap, ctx_ov, ctx_mem, cam, ctx_pe, want_pt = core_in
+        self.sig = sig
+        self.meta = (bsp, hw, overlap, want_pt)
+        clone = lambda t: None if t is None else t.detach().clone()  # noqa: E731
+        self.ins = [clone(prep), clone(ctx_ov), clone(ctx_mem), clone(cam), clone(ctx_pe)]
+        B, S, P = bsp
+        M = B * S * (P + 1)
+        dev = prep.device
+        self.x = torch.empty(round_up(M, 256), prep.shape[-1], device=dev, dtype=torch.float32)
+        self.head = head
+        self.stream = torch.cuda.Stream(dev)
+        cur = torch.cuda.current_stream(dev)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            for _ in range(2):  # settle shape-keyed caches and this stream's workspaces
+                self._run()
+        self.stream.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=self.stream):
+            self.out = self._run()
+        cur.wait_stream(self.stream)
+
+    def _run(self):
+        prep, ctx_ov, ctx_mem, cam, ctx_pe = self.ins
+        bsp, hw, overlap, want_pt = self.meta
+        return _align_core(self.head, prep, bsp, hw, overlap, ctx_ov, ctx_mem, cam, ctx_pe, want_pt, x=self.x)
+
+    def __call__(self, core_in):
+        prep, _, _, _, ctx_ov, ctx_mem, cam, ctx_pe, _ = core_in
+        for dst, src in zip(self.ins, (prep, ctx_ov, ctx_mem, cam, ctx_pe)):
+            if dst is not None:
+                dst.copy_(src)
+        self.graph.replay()
+        return tuple(None if t is None else t.clone() for t in self.out)
 
 
 def merge_results(first_chunk, second_chunk, num_overlap: int = 0, mergeDim: int = 1):
