@@ -431,21 +431,25 @@ def _recurrence_probe(pipe, step, n_chunks, t1_ms, world):
     encodes on the compute stream: t_align alone) and (b) the ring's schedule
     (align on the side stream while the next encode group runs: t_align under
     load, the regime of every W > 1 rank).  At W = 1 (b) is the W = 1 ring
-    schedule (overlap_align), whose sequence time is reported beside."""
+    schedule (overlap_align), whose sequence time is reported beside, also
+    with the encodes masked off 16 CUs (ChunkPipeline.reserve_cus)."""
     import statistics
     pipe.time_align = True
     out = {"n_chunks": n_chunks}
-    modes = (("alone", False), ("under_load", True)) if world == 1 else (("under_load", None),)
-    for name, ov_mode in modes:
-        keep = pipe.overlap_align
+    modes = ((("alone", False, 0), ("under_load", True, 0), ("under_load_reserved16", True, 16))
+             if world == 1 else (("under_load", None, None),))
+    for name, ov_mode, rsv in modes:
+        keep, keep_rsv = pipe.overlap_align, pipe.reserve_cus
         if ov_mode is not None:
             pipe.overlap_align = ov_mode
+        if rsv is not None:
+            pipe.reserve_cus = rsv
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         step()
         torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) * 1e3
-        pipe.overlap_align = keep
+        pipe.overlap_align, pipe.reserve_cus = keep, keep_rsv
         ms = pipe.align_ms()
         out["t_align_ms_%s_median" % name] = round(statistics.median(ms), 3) if ms else None
         out["t_align_ms_%s_max" % name] = round(max(ms), 3) if ms else None

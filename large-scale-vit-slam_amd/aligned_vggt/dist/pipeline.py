@@ -169,6 +169,10 @@ class ChunkPipeline:
             overlap_align = os.environ.get("VGGT_OVERLAP_ALIGN", "0") == "1"
         self.overlap_align = overlap_align
         self.time_align = time_align
+        # reserve_cus: the encodes run on a stream masked off that many CUs (spread
+        # over the XCDs), so the alignment recurrence's kernels never queue behind a
+        # full-chip encode launch; VGGT_ALIGN_RESERVE_CUS sets the default (0: off)
+        self.reserve_cus = int(os.environ.get("VGGT_ALIGN_RESERVE_CUS", "0"))
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -274,6 +278,19 @@ class ChunkPipeline:
         self.align_events = []
         if self.world == 1 and not self.overlap_align:
             mine = self._run_local(images, chunks, num_overlap, keys, memory_shape, B)
+        elif self.reserve_cus > 0 and self.device is not None and torch.device(self.device).type == "cuda":
+            enc_stream = self.__dict__.get("_enc_stream")
+            if enc_stream is None:
+                from ..runtime import cu_masked_stream, spread_cus
+                ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+                enc_stream = self._enc_stream = cu_masked_stream(self.device, spread_cus(ncu, self.reserve_cus))
+            cur = torch.cuda.current_stream(self.device)
+            enc_stream.wait_stream(cur)
+            with torch.cuda.stream(enc_stream):
+                mine = self._run_ring(images, chunks, num_overlap, keys, token_dims, memory_shape, B)
+            cur.wait_stream(enc_stream)
+            for v in mine.values():
+                _record_stream(v, cur)
         else:
             mine = self._run_ring(images, chunks, num_overlap, keys, token_dims, memory_shape, B)
         return self._gather(mine, chunks, num_overlap, B)

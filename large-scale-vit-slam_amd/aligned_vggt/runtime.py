@@ -160,3 +160,43 @@ class GraphedStep:
             self.capture()
         self.graph.replay()
         return self.out
+
+
+def spread_cus(ncu: int, n: int) -> list:
+    """n CU indices spread over the chip so that each of the 8 XCDs gets the
+    same share whether the CU-mask bits enumerate CUs XCD by XCD or
+    round-robin over the XCDs: index k*(ncu/n) + (k mod 8)."""
+    step = max(1, ncu // max(1, n))
+    return sorted({(k * step + (k % 8)) % ncu for k in range(n)})
+
+
+_HIP = None
+
+
+def cu_masked_stream(device, exclude) -> "torch.cuda.ExternalStream":
+    """A HIP stream whose kernels never run on the CUs in ``exclude``
+    (hipExtStreamCreateWithCUMask), as a torch ExternalStream.  The multi-GPU
+    pipeline encodes on such a stream so that the alignment recurrence's
+    kernels, on their own high-priority stream, always find those CUs free
+    instead of waiting behind a persistent GEMM or attention launch."""
+    import ctypes
+    global _HIP
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so")
+        _HIP.hipExtStreamCreateWithCUMask.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
+                                                      ctypes.POINTER(ctypes.c_uint32)]
+        _HIP.hipExtStreamCreateWithCUMask.restype = ctypes.c_int
+    device = torch.device(device)
+    ncu = torch.cuda.get_device_properties(device).multi_processor_count
+    words = [0xFFFFFFFF] * ((ncu + 31) // 32)
+    if ncu % 32:
+        words[-1] = (1 << (ncu % 32)) - 1
+    for i in exclude:
+        words[i // 32] &= ~(1 << (i % 32)) & 0xFFFFFFFF
+    arr = (ctypes.c_uint32 * len(words))(*words)
+    s = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        rc = _HIP.hipExtStreamCreateWithCUMask(ctypes.byref(s), len(words), arr)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+    return torch.cuda.ExternalStream(s.value, device=device)

@@ -57,10 +57,11 @@ def _model(cuda, monkeypatch, depth=4):
     return m.to(cuda).eval()
 
 
-@pytest.mark.parametrize("group", [1, 3])
-def test_overlapped_schedule_matches_sequential_loop(cuda, monkeypatch, group):
+@pytest.mark.parametrize("group,reserve", [(1, 0), (3, 0), (3, 16)])
+def test_overlapped_schedule_matches_sequential_loop(cuda, monkeypatch, group, reserve):
     """The side-stream schedule (align on its own stream, concurrent with the
-    next encode group) is bitwise equal to the sequential chunk loop."""
+    next encode group; optionally the encodes on a CU-masked stream) is bitwise
+    equal to the sequential chunk loop."""
     from aligned_vggt.dist.pipeline import ChunkPipeline, apply_sequence_to_model
     from aligned_vggt.utils.data import generate_chunks
     from aligned_vggt.utils.synthetic import synthetic_images
@@ -71,6 +72,7 @@ def test_overlapped_schedule_matches_sequential_loop(cuda, monkeypatch, group):
     ref = apply_sequence_to_model({"images": imgs}, m, [w], [ov], "chunk_overlap", None)
     P1 = 6 + (H // 14) * (W // 14)
     pipe = ChunkPipeline(m, device=cuda, gather_dense=True, encode_group=group, overlap_align=True, time_align=True)
+    pipe.reserve_cus = reserve  # > 0: encodes on a stream masked off that many CUs
     for _ in range(2):  # the second run reuses every per-stream buffer
         got = pipe.run(imgs, w, ov, token_dims=(P1, 1024), memory_shape=(1, 8, 512))
         torch.cuda.synchronize()
