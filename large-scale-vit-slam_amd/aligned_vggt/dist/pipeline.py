@@ -233,16 +233,27 @@ class ChunkPipeline:
             shapes["memory_tokens"] = mem
         return shapes
 
+    @property
+    def _comm_device(self):
+        """Where the collectives' tensors live: the GPU for RCCL; host memory
+        for gloo (CPU tests, and the single-GPU multi-process GPU test, where
+        every baton is staged through the host)."""
+        dev = torch.device(self.device) if self.device is not None else torch.device("cpu")
+        if dev.type == "cuda" and dist.is_initialized() and dist.get_backend(self.group) == "gloo":
+            return torch.device("cpu")
+        return dev
+
     def _isend(self, ctx: dict, dst: int, keys):
         """Post the baton's tensors to ``dst`` (RCCL: on its own stream, after
         the current stream's queued work); returns (works, tensors) -- the
         tensors must stay alive until the works complete."""
-        ts = [(ctx[k][-1] if isinstance(ctx[k], list) else ctx[k]).contiguous().to(self.device) for k in keys]
+        cd = self._comm_device
+        ts = [(ctx[k][-1] if isinstance(ctx[k], list) else ctx[k]).contiguous().to(cd) for k in keys]
         ops = [dist.P2POp(dist.isend, t, dst, group=self.group) for t in ts]
         return dist.batch_isend_irecv(ops), ts
 
     def _irecv(self, src: int, shapes: Dict[str, tuple]):
-        out = {k: torch.empty(shp, device=self.device, dtype=torch.float32) for k, shp in shapes.items()}
+        out = {k: torch.empty(shp, device=self._comm_device, dtype=torch.float32) for k, shp in shapes.items()}
         ops = [dist.P2POp(dist.irecv, t, src, group=self.group) for t in out.values()]
         return dist.batch_isend_irecv(ops), out
 
@@ -254,8 +265,8 @@ class ChunkPipeline:
         if self.world == 1 or self.__dict__.get("_p2p_ready"):
             return
         W, r = self.world, self.rank
-        a = torch.zeros(1, device=self.device)
-        b = torch.zeros(1, device=self.device)
+        a = torch.zeros(1, device=self._comm_device)
+        b = torch.zeros(1, device=self._comm_device)
         ops = [dist.P2POp(dist.isend, a, (r + 1) % W, group=self.group),
                dist.P2POp(dist.irecv, b, (r - 1) % W, group=self.group)]
         for w in dist.batch_isend_irecv(ops):
@@ -423,6 +434,7 @@ class ChunkPipeline:
                     if W > 1:
                         for w in works:
                             w.wait()  # RCCL: the side stream waits; gloo: the host does
+                        ctx_in = {k: v.to(self.device) for k, v in ctx_in.items()}  # no-op unless host-staged
                     else:
                         ctx_in = local
                     ctx = self._ctx_from(ctx_in, B, memory_shape)
@@ -490,7 +502,7 @@ class ChunkPipeline:
         n = len(chunks)
         slots = (n + W - 1) // W
         smax = max(len(c) for c in chunks)
-        dev = self.device if self.device is not None else torch.device("cpu")
+        dev = self._comm_device
         # small outputs, per slot: [has_depth, pose_enc B*smax*9, chunk_sim3 B*8, frame_se3 B*(smax-1)*7]
         seg = (1, B * smax * 9, B * 8, B * (smax - 1) * 7)
         per = sum(seg)
@@ -502,13 +514,15 @@ class ChunkPipeline:
             S, m = len(chunks[i]), mine[i]
             o = seg[0]
             buf[j, 0] = float(self.gather_dense and "depth" in m)
-            buf[j, o:o + B * S * 9] = m["pose_enc"].reshape(-1)
+            buf[j, o:o + B * S * 9] = m["pose_enc"].reshape(-1).to(dev)
             o += seg[1]
-            buf[j, o:o + B * 8] = m["chunk_sim3"].reshape(-1)
+            buf[j, o:o + B * 8] = m["chunk_sim3"].reshape(-1).to(dev)
             o += seg[2]
-            buf[j, o:o + B * (S - 1) * 7] = m["frame_se3"].reshape(-1)
+            buf[j, o:o + B * (S - 1) * 7] = m["frame_se3"].reshape(-1).to(dev)
         allb = torch.empty(W * slots, per, device=dev, dtype=torch.float32)
         dist.all_gather_into_tensor(allb, buf, group=self.group)
+        out_dev = torch.device(self.device) if self.device is not None else dev
+        allb = allb.to(out_dev)
         per_chunk: Dict[int, dict] = {}
         for i in range(n):
             row = allb[(i % W) * slots + i // W]
@@ -528,10 +542,11 @@ class ChunkPipeline:
                 i = r + j * W
                 if i < n:
                     S = len(chunks[i])
-                    d[j, 0, :B * S * pix] = mine[i]["depth"].reshape(-1)
-                    d[j, 1, :B * S * pix] = mine[i]["depth_conf"].reshape(-1)
+                    d[j, 0, :B * S * pix] = mine[i]["depth"].reshape(-1).to(dev)
+                    d[j, 1, :B * S * pix] = mine[i]["depth_conf"].reshape(-1).to(dev)
             alld = torch.empty(W * slots, 2, B * smax * pix, device=dev, dtype=torch.float32)
             dist.all_gather_into_tensor(alld, d, group=self.group)
+            alld = alld.to(out_dev)
             for i in range(n):
                 row = alld[(i % W) * slots + i // W]
                 S = len(chunks[i])
