@@ -14,7 +14,7 @@ torch (the reference's own Python cannot run without the absent vggt package,
 SURVEY.md §8c).  Writes one JSON (default profiles/cpu_baseline_full.json),
 which bench.py attaches to its cpu_baseline.
 
-  python scripts/cpu_baseline_full.py [--rows C1,C2] [--threads 16,0] [--runs 3] [--out PATH]
+  python scripts/cpu_baseline_full.py [--rows C1,C2] [--threads 16,0] [--runs 3] [--out PATH] [--append]
       (--threads 0 = os.cpu_count())
 """
 from __future__ import annotations
@@ -75,17 +75,38 @@ def row_c2(runs: int):
     return warm, full, "VGGT aggregator, 1 x 16 x 518^2 (DINOv2 + 24 frame/global blocks, layers 4/11/17/23)"
 
 
+def _heartbeat(state: dict) -> None:
+    """A progress line every minute (a GPU-box command that prints nothing for
+    3 minutes is taken to be hung; one C2 chunk at 16 threads takes ~8)."""
+    import threading
+
+    def beat():
+        while not state.get("done"):
+            time.sleep(60)
+            if not state.get("done"):
+                print(f"[{time.strftime('%H:%M:%S')}] still running: {state.get('what')}", flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", default="C1,C2")
     ap.add_argument("--threads", default="16,0")
     ap.add_argument("--runs", type=int, default=3)
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "cpu_baseline_full.json"))
+    ap.add_argument("--append", action="store_true", help="add rows to an existing --out file")
     a = ap.parse_args()
     res = {"host_cpu": _cpu_model(), "host_logical_cpus": os.cpu_count(), "torch": torch.__version__,
-           "procedure": f"1 warm-up (reduced-depth pass) + {a.runs} timed whole chunks, median; oracle fp32 "
-                        f"(reference numerics), random-init weights, synthetic uniform frames", "rows": {}}
+           "procedure": "1 warm-up (reduced-depth pass) + N timed whole chunks, median; oracle fp32 "
+                        "(reference numerics), random-init weights, synthetic uniform frames", "rows": {}}
+    if a.append and os.path.exists(a.out):
+        with open(a.out) as f:
+            res["rows"] = json.load(f).get("rows", {})
+    state = {"what": "setup"}
+    _heartbeat(state)
     for row in a.rows.split(","):
+        state["what"] = f"{row} setup"
         warm, full, what = {"C1": row_c1, "C2": row_c2}[row](a.runs)
         for th in (int(x) for x in a.threads.split(",")):
             th = th or (os.cpu_count() or 1)
@@ -96,16 +117,19 @@ def main():
                 tw = time.perf_counter() - t0
                 ts = []
                 for i in range(a.runs):
+                    state["what"] = f"{row} threads={th} run {i}"
                     t0 = time.perf_counter()
                     full()
                     ts.append(time.perf_counter() - t0)
                     print(f"[{time.strftime('%H:%M:%S')}] {row} threads={th} run {i}: {ts[-1]:.1f} s", flush=True)
             med = statistics.median(ts)
-            res["rows"][f"{row}_t{th}"] = {"row": row, "workload": what, "threads": th, "warmup_s": round(tw, 2),
+            res["rows"][f"{row}_t{th}"] = {"row": row, "workload": what, "threads": th, "runs": a.runs,
+                                           "warmup_s": round(tw, 2),
                                            "runs_s": [round(x, 2) for x in ts], "median_s_per_chunk": round(med, 2),
                                            "chunks_per_s": round(1.0 / med, 6)}
             with open(a.out, "w") as f:  # after every row: a killed run keeps what it measured
                 json.dump(res, f, indent=1)
+    state["done"] = True
     print(json.dumps(res))
 
 
