@@ -45,7 +45,47 @@ __global__ __launch_bounds__(256) void linear_f32_kernel(const float* __restrict
   const int mt_n = (M + 15) / 16;
   f32x4 acc[4] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
   const bool vec = ((K & 3) == 0) && ((lda & 3) == 0) && ((ldw & 3) == 0);
-  for (int k0 = kbeg; k0 < kend; k0 += 16) {
+  int k0 = kbeg;
+  if (vec) {
+    // Steady state, 64 k per iteration with no per-element guards: all of an
+    // iteration's W and A float4 loads are issued before its MFMAs (4 + 4 x mt_n
+    // loads in flight per lane instead of one round trip per 16 k -- the loop is
+    // latency-bound at skinny M).  A rows past M read row M-1: their products
+    // only reach output rows that are never stored.  The MFMA order per
+    // accumulator is the 16-k loop's, so the sums are bitwise those of the tail
+    // form below.
+    const int kv_end = kbeg + ((kend - kbeg) / 64) * 64;
+    const float* wp = W + (int64_t)nrow * ldw + 4 * q;
+    const float* ap[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) ap[mt] = A + (int64_t)min(mt * 16 + r, M - 1) * lda + 4 * q;
+    for (; k0 < kv_end; k0 += 64) {
+      f4 wv[4], av[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) wv[u] = *(const f4*)(wp + k0 + 16 * u);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        if (mt < mt_n) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) av[mt][u] = *(const f4*)(ap[mt] + k0 + 16 * u);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          if (mt >= mt_n) break;
+          f4 a4 = av[mt][u];
+          if constexpr (ACT_IN == 1) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a4[j] = a4[j] / (1.f + expf(-a4[j]));
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[j], wv[u][j], acc[mt], 0, 0, 0);
+        }
+    }
+  }
+  for (; k0 < kend; k0 += 16) {
     const int kk = k0 + 4 * q;
     f4 wv;
     if (vec && kk + 3 < kend) {
