@@ -21,7 +21,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("M,Nn,K", [(1, 8, 512), (16, 6144, 2048), (15, 9, 9), (75, 1024, 2048), (23, 100, 36),
-                                    (16, 2048, 8192), (3, 64, 1000)])
+                                    (16, 2048, 8192), (3, 64, 1000), (40, 300, 1040), (130, 72, 4160)])
 @pytest.mark.parametrize("epi,act", [(3, 0), (1, 0), (2, 0), (3, 1)])
 def test_linear_f32(N, M, Nn, K, epi, act):
     g = torch.Generator(device="cuda").manual_seed(M + Nn)
