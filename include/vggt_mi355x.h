@@ -62,12 +62,8 @@ const char* vggt_version(void);
 #define VGGT_TUNE_CONV_PF2 4     /* split-bf16 conv gather: 1 two-deep (buffer loads, default), 0 one-deep */
 #define VGGT_TUNE_ATTN16 5       /* 1: D = 64 attention on the 16x16x32 matrix-core form, 0: 32x32x16 (default),
                                     2: 16x16x32 for 4-wave (nq < 4096) launches only */
-#define VGGT_TUNE_GEMM_PIPE 6    /* persistent GEMM K-loop DMA placement bits (gemm.hip): 1 half 0 waits for its
-                                    K-tile at the end of MATH, 2 half 1 stages K-tile kt+2 inside MATH(kt),
-                                    4 half 0 issues every W piece, no READ waits on DMA,
-                                    8 half 0's epilogue overlaps half 1's last MATH segment, 16 bit 4 in the
-                                    half-K loop, 32 fragment reads before the DMA issue, 64 half 1 issues its W pieces
-                                    after its MFMAs; default 5 */
+/* (knob 6, the persistent GEMM's DMA-placement bits, is retired: its measured-best placement is the only
+   one compiled; vggt_tune(6, ...) returns VGGT_ERR_UNSUPPORTED) */
 int vggt_tune(int knob, int value);
 
 /*

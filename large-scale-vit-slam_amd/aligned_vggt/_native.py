@@ -12,6 +12,8 @@ from typing import Optional
 
 import torch
 
+from .runtime import scratch_table
+
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("VGGT_MI355X_LIB", os.path.join(_PKG_ROOT, "lib", "libvggt_mi355x.so"))
 HEADER_PATH = os.path.join(os.path.dirname(_PKG_ROOT), "include", "vggt_mi355x.h")
@@ -137,7 +139,6 @@ TUNE_ATTN_WAVES = 2
 TUNE_ATTN_VARIANT = 3
 TUNE_CONV_PF2 = 4
 TUNE_ATTN16 = 5
-TUNE_GEMM_PIPE = 6
 
 
 def tune(knob: int, value: int) -> int:
@@ -385,10 +386,11 @@ def _stream_key(device) -> tuple:
 def _split_ws(device, n_floats: int) -> torch.Tensor:
     """Grow-only per-(device, stream) scratch for split-K partial sums."""
     key = _stream_key(device)
-    t = _SPLIT_WS.get(key)
+    table = scratch_table(_SPLIT_WS, "split_k")
+    t = table.get(key)
     if t is None or t.numel() < n_floats:
         t = torch.empty(n_floats, device=key[0], dtype=torch.float32)
-        _SPLIT_WS[key] = t
+        table[key] = t
     return t
 
 
@@ -631,10 +633,11 @@ def _train_ws(device, nbytes: int) -> torch.Tensor:
     partials (stream-ordered reuse: every user consumes it before the next
     launch on the same stream; see _stream_key)."""
     key = _stream_key(device)
-    t = _TRAIN_WS.get(key)
+    table = scratch_table(_TRAIN_WS, "train")
+    t = table.get(key)
     if t is None or t.numel() * 4 < nbytes:
         t = torch.empty((nbytes + 3) // 4 + 64, device=key[0], dtype=torch.float32)
-        _TRAIN_WS[key] = t
+        table[key] = t
     return t
 
 

@@ -104,15 +104,18 @@ class AlignmentHead(nn.Module):
 
     # ------------------------------------------------------------------
     def _rope2d(self, h: int, w: int, device) -> RopeTables:
+        """2-D RoPE tables per patch grid, kept for every grid seen: a HIP graph
+        captured for one grid reads them on each replay, so they must outlive
+        a switch to another grid (a one-entry cache freed them under it)."""
+        cache = self.__dict__.setdefault("_mi355x_rope2d", {})
         key = (h, w, str(device))
-        c = self.__dict__.get("_mi355x_rope2d")
-        if c is None or c[0] != key:
+        c = cache.get(key)
+        if c is None:
             yy, xx = torch.meshgrid(torch.arange(h), torch.arange(w), indexing="ij")
             pos = torch.stack([yy.reshape(-1), xx.reshape(-1)], -1) + 1
             pos = torch.cat([torch.zeros(self.patch_start_idx, 2, dtype=pos.dtype), pos], 0)
-            c = (key, RopeTables(pos, self.embed_dim // self.num_heads, float(self.rope_freq), device))
-            self.__dict__["_mi355x_rope2d"] = c
-        return c[1]
+            c = cache[key] = RopeTables(pos, self.embed_dim // self.num_heads, float(self.rope_freq), device)
+        return c
 
     def _i32(self, pos: torch.Tensor, device) -> torch.Tensor:
         """Device int32 copy of a small host position vector, cached per value

@@ -23,7 +23,7 @@ from ..backbone.camera_head import CameraHead
 from ..backbone.dpt_head import DPTHead
 from ..backbone.track_head import TrackHead
 from ..heads.alignment_head import AlignmentHead
-from ..runtime import round_up
+from ..runtime import private_scratch, round_up
 from ..utils.data import extri_to_pose_encoding, pose_encoding_to_extri
 from ..utils.geometry import averagePoseEncodings, closed_form_inverse_se3
 from ..utils.pose_enc import extri_intri_to_pose_encoding, pose_encoding_to_extri_intri
@@ -318,9 +318,11 @@ def _align_core(head, prep, bsp, hw, overlap, ctx_ov, ctx_mem, cam, ctx_pe, want
 class _AlignGraph:
     """One HIP graph of _align_core for one input shape.  Inputs are copied
     into static buffers, the graph replays on the current stream, outputs are
-    cloned out (the next replay overwrites them).  Captured on a stream of its
-    own: the per-(device, stream) workspaces and split-K scratch the kernels
-    read are then that stream's alone and never grow (and move) after capture.
+    cloned out (the next replay overwrites them).  Warm-ups and capture run
+    inside private_scratch: the workspaces and split-K slabs the kernels read
+    belong to this object and never grow (and move) after capture -- the
+    shared per-(device, stream) tables would not do, capture streams come from
+    torch's pool and are handed to later graphs too.
     Parameter values are baked in through the cached operand packs -- the
     owner re-captures when any parameter's (storage, version) changes."""
 
@@ -336,15 +338,17 @@ class _AlignGraph:
         self.x = torch.empty(round_up(M, 256), prep.shape[-1], device=dev, dtype=torch.float32)
         self.head = head
         self.stream = torch.cuda.Stream(dev)
+        self.scratch = {}  # the graph's own workspaces / split-K slabs (private_scratch)
         cur = torch.cuda.current_stream(dev)
         self.stream.wait_stream(cur)
-        with torch.cuda.stream(self.stream):
-            for _ in range(2):  # settle shape-keyed caches and this stream's workspaces
-                self._run()
-        self.stream.synchronize()
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, stream=self.stream):
-            self.out = self._run()
+        with private_scratch(self.scratch):
+            with torch.cuda.stream(self.stream):
+                for _ in range(2):  # settle shape-keyed caches and the workspaces' sizes
+                    self._run()
+            self.stream.synchronize()
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph, stream=self.stream):
+                self.out = self._run()
         cur.wait_stream(self.stream)
 
     def _run(self):

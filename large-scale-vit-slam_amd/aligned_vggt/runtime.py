@@ -12,6 +12,8 @@ workspaces.
 """
 from __future__ import annotations
 
+import contextlib
+import threading
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -55,11 +57,38 @@ def f32_param(mod: nn.Module, name: str, fill: Optional[float] = None, n: int = 
     return p.detach().float().contiguous() if p.dtype != torch.float32 or not p.is_contiguous() else p.detach()
 
 
+_SCOPE = threading.local()
+
+
+@contextlib.contextmanager
+def private_scratch(store: dict):
+    """Route every grow-only scratch lookup (Workspace, the split-K and
+    training-reduction slabs of _native) made inside the block to ``store``
+    instead of the shared per-(device, stream) tables.  A HIP graph's capture
+    and its warm-ups run inside one, with a store the graph object owns: the
+    pointers the graph bakes in then belong to it alone.  Shared tables are
+    keyed by stream, and torch hands capture streams out of a small pool, so a
+    later graph -- or eager work -- on the same pool stream could otherwise
+    grow (re-allocate) a buffer an earlier graph still replays into."""
+    prev = getattr(_SCOPE, "store", None)
+    _SCOPE.store = store
+    try:
+        yield store
+    finally:
+        _SCOPE.store = prev
+
+
+def scratch_table(shared: dict, kind: str) -> dict:
+    """The table scratch of ``kind`` lives in: the active private store's, else ``shared``."""
+    st = getattr(_SCOPE, "store", None)
+    return shared if st is None else st.setdefault(kind, {})
+
+
 class Workspace:
     """Named, grow-only device buffers: one set per (device, stream), so work
     queued on two streams at once (the multi-GPU pipeline aligns chunk i on a
     side stream while the compute stream encodes chunk i + W) never shares a
-    scratch buffer."""
+    scratch buffer; a captured graph's own set inside ``private_scratch``."""
 
     _per_device: Dict[tuple, "Workspace"] = {}
 
@@ -76,9 +105,10 @@ class Workspace:
             key = (device, torch.cuda.current_stream(device).stream_id)
         else:
             key = (device, 0)
-        ws = cls._per_device.get(key)
+        table = scratch_table(cls._per_device, "workspace")
+        ws = table.get(key)
         if ws is None:
-            ws = cls._per_device[key] = Workspace(device)
+            ws = table[key] = Workspace(device)
         return ws
 
     def buf(self, name: str, rows: int, cols: int, dtype=torch.float32) -> torch.Tensor:
@@ -137,21 +167,23 @@ class GraphedStep:
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.graph = None
         self.out = None
+        self.scratch = {}  # this graph's own workspaces (private_scratch)
 
     def capture(self) -> None:
         if self.device.type != "cuda":
             raise RuntimeError("GraphedStep: HIP graphs need a HIP device")
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(s):
-            for _ in range(self.warmup):
-                self.fn()
-        s.synchronize()
-        for m in self.modules:
-            drop_weight_caches(m)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
-            self.out = self.fn()
+        with private_scratch(self.scratch):
+            with torch.cuda.stream(s):
+                for _ in range(self.warmup):
+                    self.fn()
+            s.synchronize()
+            for m in self.modules:
+                drop_weight_caches(m)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                self.out = self.fn()
         torch.cuda.current_stream(self.device).wait_stream(s)
         self.graph = g
 

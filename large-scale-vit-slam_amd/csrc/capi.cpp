@@ -21,9 +21,6 @@ int g_vggt_attn_variant = env_or("VGGT_ATTN_VARIANT", 33);
 // (profiles/r6d), frame-only faster (r7b: step 98.9-99.0 -> 98.3 ms)
 int g_vggt_attn16 = env_or("VGGT_ATTN16", 2);
 int g_vggt_conv_pf2 = env_or("VGGT_CONV_PF2", 1);
-// 5: half 0 issues every W piece and no READ segment waits on DMA in the whole-K-tile loop
-// (profiles/r7c/r7d: aggregator step 102.4 -> 99.3 ms with the frame-only 16x16 attention, same box)
-int g_vggt_gemm_pipe = env_or("VGGT_GEMM_PIPE", 5);
 
 extern "C" int vggt_tune(int knob, int value) {
   int prev;
@@ -59,11 +56,6 @@ extern "C" int vggt_tune(int knob, int value) {
       if (value != 0 && value != 1) return VGGT_ERR_UNSUPPORTED;
       prev = g_vggt_conv_pf2;
       g_vggt_conv_pf2 = value;
-      return prev;
-    case VGGT_TUNE_GEMM_PIPE:
-      if (value < 0 || value > 127) return VGGT_ERR_UNSUPPORTED;
-      prev = g_vggt_gemm_pipe;
-      g_vggt_gemm_pipe = value;
       return prev;
     default: return VGGT_ERR_UNSUPPORTED;
   }

@@ -1229,33 +1229,6 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
     __builtin_amdgcn_s_setprio(0);
   };
 
-  // math2 with (when `st`) K-tile skt's DMA pieces (W, then A) spread over the MFMA
-  // stream: piece p after MFMA (p + 1) * TOT / (LPS + 1) - 1, behind a wave-uniform
-  // branch so the register allocation is math2's
-  auto math2_stage = [&](bool st, int sbuf, int skt) {
-    if constexpr (!FK) return;
-    constexpr int TOT = 2 * C::MI * C::NI;
-    const uint32_t b = lds0 + sbuf * C::BUF;
-    const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(skt * PBK * 2));
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < TOT; ++i) {
-      const int h = i / (C::MI * C::NI), r = i % (C::MI * C::NI), mi = r / C::NI, ni = r % C::NI;
-      acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h ? wf2[ni] : wf[ni], h ? af2[mi] : af[mi], acc[ni][mi], 0, 0, 0);
-#pragma unroll
-      for (int p = 0; p < LPS; ++p)
-        if (i == (p + 1) * TOT / (LPS + 1) - 1) {
-          __builtin_amdgcn_sched_barrier(0);
-          if (st) {
-            if (p < C::WL) dma16s(rw, woff[p], soff, b + C::ABYTES + (wave * C::WL + p) * 1024);
-            else dma16s(ra, aoff[p - C::WL], soff, b + (wave * C::AL + p - C::WL) * 1024);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-    __builtin_amdgcn_s_setprio(0);
-  };
-
   int tile = blockIdx.x;
   if (tile >= ntiles) return;
   // prologue: the first tile's K-tiles 0 and 1
@@ -1279,124 +1252,48 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
       for (int j = 0; j < C::MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (wm == 1) asm volatile("s_barrier" ::: "memory");  // stagger the second M half by one segment
     if constexpr (FK) {
-      // DMA placement (sched bits 9-10, VGGT_TUNE_GEMM_PIPE): with bit 9 half 0 no longer waits for the
-      // K-tile kt+1 pieces it issued at READ(kt) before READ(kt)'s barrier but at the end of MATH(kt)
-      // (half 0 reads them first, at READ(kt+1)); with bit 10 half 1 issues no DMA in its READ
-      // segments and instead stages K-tile kt+2 inside MATH(kt), one piece per MFMA group (the buffer
-      // of K-tile kt is free by then: both halves read it in the two segments before), waiting for
-      // them at the end of its next READ.  Either way every wait covers pieces issued at least one
-      // segment earlier, so no READ segment carries a DMA round trip.
-      // Bit 11 (with bit 9): half 0 issues every W piece of K-tile kt+1 (its own and half 1's rows,
-      // the latter 128 rows on through the scalar offset) and half 1 only its A pieces, which it then
-      // waits for at the end of MATH(kt) like half 0 -- no READ segment waits on DMA at all.
-      // the default placement (bit 11) as its own copy of the loop, with no runtime
-      // placement branches in it
-      auto fk_loop = [&](auto wallc, auto rfc) {
-        constexpr bool WALL = decltype(wallc)::value;
-        constexpr bool rfirst = decltype(rfc)::value;
-        const bool dh0 = WALL || (((sched >> 9) & 1) && wm == 0);
-        const bool mh1 = !WALL && ((sched >> 10) & 1) && wm == 1;
-        for (int kt = 0; kt < nk; ++kt) {
-          const int buf = (b0 + kt) & 1;
-          const bool pf = kt >= 1 && kt + 1 < nk;
-          // READ(kt): K-tile kt+1's DMA pieces, then both K halves' fragments
-          if constexpr (WALL) {
-            // sched bit 14: the fragment reads before the DMA issue (the reads then land while
-            // the pieces issue)
-            if constexpr (rfirst) {
-              read_frags(buf, 0);
-              read_frags2(buf);
-            }
-            if (pf) {
-              if (wm == 0) {
-                stage_w(buf ^ 1, kt + 1);
-                stage_w2(buf ^ 1, kt + 1);
-              }
-              stage_a(buf ^ 1, kt + 1);
-            }
-            if constexpr (!rfirst) {
-              read_frags(buf, 0);
-              read_frags2(buf);
-            }
-          } else {
-            if (pf && !mh1) {
-              stage_w(buf ^ 1, kt + 1);
-              stage_a(buf ^ 1, kt + 1);
-            }
-            read_frags(buf, 0);
-            read_frags2(buf);
-          }
-          const bool lead = WALL ? !(wm == 1 && kt == 0) : dh0;  // waits move to the end of MATH
-          if (lead) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-          else if (!WALL && pf && !mh1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::AL) : "memory");
-          else if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NST) : "memory");
-          else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-          __builtin_amdgcn_sched_barrier(0);
-          if constexpr (WALL) math2();
-          else math2_stage(mh1 && kt + 2 < nk, buf, kt + 2);
-          __builtin_amdgcn_sched_barrier(0);
-          if (lead) {
-            if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NST) : "memory");
-            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-          } else if (!WALL && pf && !mh1) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-          else asm volatile("s_barrier" ::: "memory");
-        }
-      };
-      // sched bit 15: half 0 issues its own W and A pieces of K-tile kt+1 at READ(kt) and waits for them at
-      // the end of MATH(kt); half 1 issues its W pieces of K-tile j+2 after the MFMAs of MATH(j) (the buffer
-      // of K-tile j is free by then) and its A pieces of K-tile kt+1 at READ(kt), and waits for the W pieces
-      // at the end of READ(kt) -- a segment after issue -- and for the A pieces at the end of MATH(kt).  Each
-      // READ segment issues at most eight pieces instead of half 0's twelve.
-      auto fk_w1m = [&]() {
-        for (int kt = 0; kt < nk; ++kt) {
-          const int buf = (b0 + kt) & 1;
-          const bool pf = kt >= 1 && kt + 1 < nk;
-          if (pf) {
-            if (wm == 0) stage_w(buf ^ 1, kt + 1);
-            stage_a(buf ^ 1, kt + 1);
-          }
-          read_frags(buf, 0);
-          read_frags2(buf);
-          if (wm == 0) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-          else if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NST) : "memory");
-          else if (pf) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::AL) : "memory");
-          else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-          __builtin_amdgcn_sched_barrier(0);
-          math2();
-          __builtin_amdgcn_sched_barrier(0);
-          const bool w1 = wm == 1 && kt + 2 < nk;
-          if (w1) stage_w(buf, kt + 2);
+      // whole-K-tile loop.  DMA placement: half 0 issues every W piece of K-tile kt+1 (its own
+      // rows and, through the scalar offset, half 1's 128 rows on) and half 1 only its A pieces;
+      // both wait for them at the end of MATH(kt), so no READ segment waits on DMA
+      // (profiles/r7c-r7d: aggregator step 102.4 -> 99.3 ms against waiting at the end of READ;
+      // the other placements measured -- half 0 deferring only its own wait, half 1 staging
+      // K-tile kt+2 inside MATH, half 1 issuing its W pieces after its MFMAs, fragment reads
+      // ahead of the DMA issue -- were slower and are gone)
+      for (int kt = 0; kt < nk; ++kt) {
+        const int buf = (b0 + kt) & 1;
+        const bool pf = kt >= 1 && kt + 1 < nk;
+        // READ(kt): K-tile kt+1's DMA pieces, then both K halves' fragments
+        if (pf) {
           if (wm == 0) {
-            if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NST) : "memory");
-            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-          } else if (w1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(C::WL) : "memory");
-          else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+            stage_w(buf ^ 1, kt + 1);
+            stage_w2(buf ^ 1, kt + 1);
+          }
+          stage_a(buf ^ 1, kt + 1);
         }
-      };
-      if ((sched >> 15) & 1) {
-        fk_w1m();
-      } else if ((sched >> 11) & 1) {
-        if ((sched >> 14) & 1) fk_loop(std::true_type{}, std::true_type{});
-        else fk_loop(std::true_type{}, std::false_type{});
-      } else {
-        fk_loop(std::false_type{}, std::false_type{});
+        read_frags(buf, 0);
+        read_frags2(buf);
+        // half 1's K-tile 0 was staged before the loop: it waits for it here
+        const bool lead = !(wm == 1 && kt == 0);
+        if (lead) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else if (stores_out) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NST) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        math2();
+        __builtin_amdgcn_sched_barrier(0);
+        if (lead) {
+          if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NST) : "memory");
+          else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        } else {
+          asm volatile("s_barrier" ::: "memory");
+        }
       }
     } else {
-    // (sched bit 13; measured slower for the fused qkv GEMM: 147.3-148.6 -> 150.4-151.2 us, r7d)
-    const bool wall_h = (sched >> 13) & 1;
     for (int kt = 0; kt < nk; ++kt) {
       const int buf = (b0 + kt) & 1;
       const bool pf = kt >= 1 && kt + 1 < nk;  // this step issues K-tile kt+1 (K-tile 1 was issued ahead)
       // READ(kt, 0): K-tile kt+1's DMA (split: its W half), this step's fragments
       if (pf) {
-        if (split && wall_h) {
-          // (sched bit 13) half 0 issues every W piece of K-tile kt+1 and waits for
-          // them at the end of MATH(kt, 1), three segments on; half 1 issues none
-          if (wm == 0) {
-            stage_w(buf ^ 1, kt + 1);
-            stage_w2(buf ^ 1, kt + 1);
-          }
-        } else if (split) stage_w(buf ^ 1, kt + 1);
+        if (split) stage_w(buf ^ 1, kt + 1);
         else stage(buf ^ 1, kt + 1);
       }
       read_frags(buf, 0);
@@ -1411,8 +1308,7 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
       if (pf && split) {
         stage_a(buf ^ 1, kt + 1);
         read_frags(buf, 1);
-        if (wall_h) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::AL) : "memory");
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(C::AL) : "memory");
       } else {
         read_frags(buf, 1);
         if (kt == 0 && stores_out) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NST) : "memory");
@@ -1425,16 +1321,8 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
       else asm volatile("s_barrier" ::: "memory");
     }
     }
-    // sched bit 12: half 0 runs its epilogue (and stages the next tile's first K-tiles) while
-    // half 1 is still in MATH(nk-1), and takes the balancing barrier after it.  Both
-    // buffers are free then: every READ segment ends with lgkmcnt(0) before its barrier,
-    // and half 0 has passed the barrier that ends half 1's last READ.  Measured slower
-    // (r7d: fc1 + GELU 190 -> 215 us, fused qkv 151 -> 158 us, aggregator step +1.5 ms).
-    const bool early = (sched >> 12) & 1;
-    if (!early) {
-      if (wm == 0) asm volatile("s_barrier" ::: "memory");  // balance the stagger
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every read of both buffers retired
-    }
+    if (wm == 0) asm volatile("s_barrier" ::: "memory");  // balance the stagger
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every read of both buffers retired
 
     // RESID: this tile's fp32 residual rows, loaded BEFORE the next tile's DMA
     // (the compiler's waits for them then never cover the younger DMA)
@@ -1633,7 +1521,6 @@ __global__ __launch_bounds__(PNT, 1) void gemm_ppp_kernel(const bf16_t* __restri
         }
       }
     }
-    if (early && wm == 0) asm volatile("s_barrier" ::: "memory");  // balance: half 1's MATH(nk-1) ends
     if (!more) break;
     // own K-tile 0 of the next tile landed (K-tile 1 and the stores may still
     // be in flight), then everyone's
@@ -1706,7 +1593,7 @@ int launch_ppp_fk(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, in
     const char* d = getenv("VGGT_GEMM_SPLITDMA");
     return (e ? atoi(e) & 255 : 4) | (d && !atoi(d) ? 0 : 256);
   }();
-  gemm_ppp_kernel<EPI, BMT, FK><<<nwg, PNT, lds, s>>>(a, lda, w, ldw, M, N, K, ep, sched | (g_vggt_gemm_pipe & 127) << 9);
+  gemm_ppp_kernel<EPI, BMT, FK><<<nwg, PNT, lds, s>>>(a, lda, w, ldw, M, N, K, ep, sched);
   return VGGT_OK;
 }
 

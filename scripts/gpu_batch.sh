@@ -20,8 +20,8 @@ step() {  # step NAME SECONDS CMD...
   return $rc
 }
 if [ "$WHAT" = tests ] || [ "$WHAT" = all ]; then
-  step pytest 900 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_ring.py tests/test_gpu_align.py tests/test_gpu_small_kernels.py \
-    tests/test_gpu_model.py tests/test_gpu_train.py tests/test_gpu_aggregator.py -x -v -s --timeout 500 \
+  step pytest 1000 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_ring.py tests/test_gpu_align.py tests/test_gpu_small_kernels.py \
+    tests/test_gpu_model.py tests/test_gpu_train.py tests/test_gpu_aggregator.py tests/test_gpu_kernels.py -x -v -s --timeout 500 \
     --timeout-method thread || exit $?
 fi
 if [ "$WHAT" = benches ] || [ "$WHAT" = all ]; then

@@ -52,8 +52,8 @@ def test_tune_knobs_range_and_restore():
     if not os.path.exists(N.LIB_PATH):
         pytest.skip("library not built")
     lib = N.lib()
-    for knob, good, bad in ((N.TUNE_GEMM_PIPE, (0, 1, 5, 37, 64, 127), (-1, 128)),
-                            (N.TUNE_ATTN16, (0, 1, 2), (3, -1)),
+    assert lib.vggt_tune(6, 5) < 0  # the retired GEMM DMA-placement knob
+    for knob, good, bad in ((N.TUNE_ATTN16, (0, 1, 2), (3, -1)),
                             (N.TUNE_ATTN_WAVES, (2, 4, 8), (3, 16))):
         first = lib.vggt_tune(knob, good[0])
         assert first >= 0
@@ -66,9 +66,6 @@ def test_tune_knobs_range_and_restore():
             assert lib.vggt_tune(knob, prev) == prev  # a rejected value changed nothing
         lib.vggt_tune(knob, first)
     # the defaults the round-3 measurements chose, unless the environment overrides them
-    if "VGGT_GEMM_PIPE" not in os.environ:
-        p = lib.vggt_tune(N.TUNE_GEMM_PIPE, 5)
-        assert p == 5
     if "VGGT_ATTN16" not in os.environ:
         p = lib.vggt_tune(N.TUNE_ATTN16, 2)
         assert p == 2

@@ -206,6 +206,37 @@ def test_feature_aligned_given_oracle_tokens(models, monkeypatch):
         assert _rel(a, b) < 1e-3
 
 
+def test_align_graph_survives_other_shapes(models):
+    """A captured alignment-recurrence graph (featureAligned_vggt._AlignGraph)
+    replayed after more graphs than torch's 32-stream pool holds were captured
+    for larger patch grids, and after an eager run on yet another grid, must
+    still give the eager recurrence's result: every table and scratch slab the
+    graph reads has to outlive those (a one-entry RoPE-table cache and
+    stream-keyed scratch shared with later captures did not)."""
+    m, _ = models
+    from aligned_vggt.models.featureAligned_vggt import _align_core
+    head = m.alignment_head
+    gen = torch.Generator().manual_seed(3)
+
+    def core_in(H, W, S=4):
+        P = head.patch_start_idx + (H // 14) * (W // 14)
+        toks = (torch.randn(1, S, P, 2 * 1024, generator=gen) * 0.5).cuda()
+        prep = head.prepare_infer(toks, (H, W))
+        return (prep[:S * (P + 1)].view(1, S * (P + 1), -1), (1, S, P), (H, W), 2, None, None, None, None, False)
+
+    a = core_in(42, 70)
+    ref = [t.clone() for t in _align_core(head, *a) if t is not None]
+    first = [t for t in m._align_graph(a) if t is not None]
+    for k in range(6, 6 + 34):
+        m._align_graph(core_in(42, 14 * k))
+    _align_core(head, *core_in(28, 28))
+    again = [t for t in m._align_graph(a) if t is not None]
+    torch.cuda.synchronize()
+    for r, f, g in zip(ref, first, again):
+        assert _rel(f, r) < 1e-6, _rel(f, r)
+        assert _rel(g, r) < 1e-6, _rel(g, r)
+
+
 def _synthetic_w2c(S, seed=7):
     """Smooth synthetic trajectory (yaw random walk, ~1 unit forward per frame), w2c (1,S,3,4)."""
     g = torch.Generator().manual_seed(seed)

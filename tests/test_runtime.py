@@ -1,0 +1,43 @@
+"""Host logic of the scratch tables (aligned_vggt/runtime.py): private_scratch
+routes every grow-only scratch lookup -- Workspace, the split-K and training
+reduction slabs -- to the store a captured graph owns, and restores the shared
+tables on exit (also when nested or on error).  CPU tensors only."""
+import pytest
+import torch
+
+
+def test_private_scratch_routes_and_restores():
+    from aligned_vggt import _native as N
+    from aligned_vggt.runtime import Workspace, private_scratch
+    cpu = torch.device("cpu")
+    shared_ws = Workspace.get(cpu)
+    shared_split = N._split_ws(cpu, 16)
+    store, inner = {}, {}
+    with private_scratch(store):
+        ws = Workspace.get(cpu)
+        assert ws is not shared_ws and store["workspace"][(cpu, 0)] is ws
+        t = N._split_ws(cpu, 32)
+        assert t is not shared_split and store["split_k"][(cpu, 0)] is t
+        r = N._train_ws(cpu, 100)
+        assert store["train"][(cpu, 0)] is r
+        with private_scratch(inner):
+            assert Workspace.get(cpu) is not ws and "workspace" in inner
+        assert Workspace.get(cpu) is ws  # the outer store again
+        assert N._split_ws(cpu, 8) is t  # grow-only: the bigger slab is reused
+    assert Workspace.get(cpu) is shared_ws
+    assert N._split_ws(cpu, 16) is shared_split
+    with pytest.raises(RuntimeError):
+        with private_scratch({}):
+            raise RuntimeError("boom")
+    assert Workspace.get(cpu) is shared_ws
+
+
+def test_workspace_buffers_grow_only():
+    from aligned_vggt.runtime import Workspace, private_scratch
+    with private_scratch({}):
+        ws = Workspace.get("cpu")
+        a = ws.buf("x", 4, 8)
+        b = ws.buf("x", 2, 8)
+        assert b.data_ptr() == a.data_ptr()
+        c = ws.buf("x", 8, 8)
+        assert c.shape == (8, 8) and c.data_ptr() != a.data_ptr()
