@@ -366,7 +366,7 @@ def test_dpt_matches_transformers_depth_anything(golden, monkeypatch, conv, reor
     monkeypatch.setattr(D, "REORDER_OUT_CONV", reorder)
     g = golden("dpt_hf")
     sd = {k[3:]: torch.from_numpy(np.ascontiguousarray(v)) for k, v in g.items() if k.startswith("sd.")}
-    head = D.DPTHead(dim_in=64, features=64, out_channels=(32, 32, 64, 64), output_dim=2, activation="exp",
+    head = D.DPTHead(dim_in=256, features=64, out_channels=(32, 32, 64, 64), output_dim=2, activation="exp",
                      pos_embed=False, intermediate_layer_idx=range(4))
     head.load_state_dict(sd, strict=True)
     head = head.cuda()
