@@ -519,319 +519,6 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// D = 64, 8 waves: the two wave halves staggered by one segment (variants
-// 289-291).  The 8-wave form above runs all 8 waves in lockstep through one
-// barrier per tile, so the two waves that share a SIMD issue their 16 MFMAs at
-// the same time (the matrix pipe runs both back to back) and then their
-// softmax at the same time (the pipe idles while both contend for the vector
-// issue port): ~1,000 cycles per wave-tile for 512 cycles of MFMA.  Here each
-// wave's tile loop is two segments -- M(t): P.V of tile t-1 and QK^T of tile t
-// (16 MFMAs); V(t): the softmax of tile t (exp, sums, bf16 pack) -- and waves
-// 4-7 run one segment behind waves 0-3 (one extra barrier before their loop,
-// one after the other half's), so on every SIMD one wave's MFMA segment pairs
-// with its partner's VALU segment (MI355X_MICROARCH.md 'Two waves per SIMD').
-// Tile t+1 is staged by LDS-DMA at global segment 2t and waited for at the end
-// of segment 2t+1; tile t is read from segment 2t (K, first half) to 2t+3 (V,
-// second half), so three K|V slots (48 KiB) rotate.  The arithmetic is variant
-// 33's step for step (offset-free softmax, same MFMA order per accumulator),
-// so the output equals it bit for bit.
-// PM: 0 = waves 4-7 at static priority 1 (as the lockstep form), 1 = no
-// priority, 2 = priority 1 in M segments only (the MFMA issue is never held
-// behind the partner's softmax).
-template <int PM>
-__global__ __launch_bounds__(512, 1) void attn_stag_kernel(AttnArgs a) {
-  constexpr int D = 64, BQ = 256, ROWB = 128, TILEB = BKV * ROWB, NKS = 4, NDB = 2, CPR = 8;
-  __shared__ __attribute__((aligned(16))) char smem[3 * 2 * TILEB];
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int hl = lane >> 5;
-  const int half = wave >> 2;
-  if constexpr (PM == 0) {
-    if (half) __builtin_amdgcn_s_setprio(1);
-  }
-  const int nqb = (a.nq + BQ - 1) / BQ;
-  const int bid = xcd_remap(blockIdx.x, nqb * a.heads * a.batch);
-  const int qb = bid % nqb;
-  const int bh = bid / nqb;
-  const int h = bh % a.heads;
-  const int b = bh / a.heads;
-  const bf16_t* qp = a.q + (int64_t)b * a.qbs * a.ldq + h * D;
-  const bf16_t* kp = a.k + (int64_t)b * a.kbs * a.ldk + h * D;
-  const bf16_t* vp = a.v + (int64_t)b * a.vbs * a.ldv + h * D;
-
-  // Q fragments (B operand of S^T = K Q^T), prescaled into log2 units
-  const int qrow = qb * BQ + wave * 32 + (lane & 31);
-  const int qr = min(qrow, a.nq - 1);
-  bf16x8 qf[NKS];
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) qf[ks] = *(const bf16x8*)(qp + (int64_t)qr * a.ldq + ks * 16 + 8 * hl);
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qf[ks][j] = (__bf16)((float)qf[ks][j] * a.c);
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) asm volatile("" : "+v"(qf[ks]));
-
-  // one 1-KiB DMA piece of K and one of V per wave per tile (rows 8 wave .. +7)
-  const int drow = wave * 8 + lane / CPR, dcp = lane % CPR;
-  const uint32_t koff = (uint32_t)(drow * a.ldk + k_swz<D>(drow, dcp) * 8) * 2u;
-  const uint32_t voff = (uint32_t)(drow * a.ldv + v_swz<D>(drow, dcp) * 8) * 2u;
-  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem)) + wave * 1024;
-  const int kstep = BKV * (int)a.ldk * 2, vstep = BKV * (int)a.ldv * 2;
-  const int kbytes = a.nk * (int)a.ldk * 2, vbytes = a.nk * (int)a.ldv * 2;
-  const int nt = (a.nk + BKV - 1) / BKV;
-  auto stage = [&](int slot, int t) {
-    const int ko = kstep * t, vo = vstep * t;
-    const int32x4 kr = make_rsrc((const char*)kp + ko, (uint32_t)max(kbytes - ko, 0));
-    const int32x4 vr = make_rsrc((const char*)vp + vo, (uint32_t)max(vbytes - vo, 0));
-    const uint32_t d = lds0 + slot * 2 * TILEB;
-    dma16(kr, koff, d);
-    dma16(vr, voff, d + TILEB);
-  };
-
-  uint32_t ka[NKS];
-  {
-    const int key = lane & 31;
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) ka[ks] = key * ROWB + (k_swz<D>(key, 2 * ks + hl) << 4);
-  }
-  uint32_t va[NDB];
-  {
-    const int g = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
-    const int r0 = 4 * hl + qq;
-#pragma unroll
-    for (int db = 0; db < NDB; ++db) {
-      const int col = db * 32 + 16 * g + 4 * pp;
-      va[db] = TILEB + r0 * ROWB + (v_swz<D>(r0, col >> 3) << 4) + (col & 7) * 2;
-    }
-  }
-
-  f32x16 o[NDB];
-#pragma unroll
-  for (int i = 0; i < NDB; ++i) o[i] = f32x16{};
-  constexpr float M_UNSET = -1e30f;
-  float m_run = M_UNSET, l_run = 0.f;
-  float limv = 256.0f;
-  bool zero_off = false;
-  const float c = a.c;
-  f32x16 s[2];      // S^T of the tile between its M and V segments
-  bf16x8 pf[2][2];  // P^T of the tile between its V segment and the next M
-
-  auto qk = [&](auto slotc) {
-    constexpr int SL = decltype(slotc)::value;
-    const char* base = smem + SL * 2 * TILEB;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      s[kb] = f32x16{};
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        const bf16x8 kf = *(const bf16x8*)(base + ka[ks] + kb * 32 * ROWB);
-        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kb], 0, 0, 0);
-      }
-    }
-  };
-  auto pv = [&](auto slotc) {
-    constexpr int SL = decltype(slotc)::value;
-    const char* base = smem + SL * 2 * TILEB;
-#pragma unroll
-    for (int db = 0; db < NDB; ++db)
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-          const char* p0 = base + va[db] + (kb * 32 + 16 * ss) * ROWB;
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)LDS_PTR(p0));
-          const s16x4 hi =
-              __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)LDS_PTR(p0 + 8 * ROWB));
-          const bf16x8 vf = __builtin_bit_cast(bf16x8, (s16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-          o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kb][ss], o[db], 0, 0, 0);
-        }
-  };
-  // the raw scores again (rare path), through an opaque LDS offset as in attn_fwd_kernel
-  auto qk_again = [&](auto slotc) {
-    constexpr int SL = decltype(slotc)::value;
-    uint32_t opq = SL * 2 * TILEB;
-    asm volatile("" : "+v"(opq));
-    const char* base = smem + opq;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      s[kb] = f32x16{};
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        const bf16x8 kf = *(const bf16x8*)(base + ka[ks] + kb * 32 * ROWB);
-        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kb], 0, 0, 0);
-      }
-    }
-  };
-  // softmax of tile t (variant 33's offset-free step): s -> pf, l_run
-  auto soft = [&](auto slotc, int t) {
-    const int kv0 = t * BKV;
-    auto mask = [&]() {
-      if (kv0 + BKV > a.nk) {
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = kv0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-            if (key >= a.nk) s[kb][r] = -INFINITY;
-          }
-      }
-    };
-    mask();
-    float rs = 0.f;
-    auto exps = [&](auto shc) {
-      constexpr bool shifted = decltype(shc)::value;
-      rs = 0.f;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-          bf16x8 tv;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            float x = s[kb][8 * ss + j];
-            if constexpr (shifted) x -= m_run;
-            const float p = __builtin_amdgcn_exp2f(x);
-            rs += p;
-            tv[j] = (__bf16)p;
-          }
-          pf[kb][ss] = tv;
-        }
-    };
-    if (zero_off) exps(std::false_type{});
-    else exps(std::true_type{});
-    if (__builtin_amdgcn_ballot_w64(!(rs <= limv)) != 0) {
-      qk_again(slotc);
-      mask();
-      float mx = fmaxf(s[0][0], s[0][1]);
-#pragma unroll
-      for (int r = 2; r < 16; r += 2) mx = fmaxf(fmaxf(mx, s[0][r]), s[0][r + 1]);
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) mx = fmaxf(fmaxf(mx, s[1][r]), s[1][r + 1]);
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-      const float lim = m_run == 0.f ? 60.f : THR;
-      float m_new = m_run;
-      if (m_run == M_UNSET) m_new = fabsf(mx) <= 60.f ? 0.f : mx;
-      else if (mx > m_run + (lim - 5.f)) m_new = mx;
-      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-      m_run = m_new;
-      limv = m_run == 0.f ? 0x1p60f : 256.0f;
-      zero_off = __builtin_amdgcn_ballot_w64(m_run != 0.f) == 0;
-      l_run *= alpha;
-#pragma unroll
-      for (int db = 0; db < NDB; ++db) o[db] *= alpha;
-      exps(std::true_type{});
-    }
-    l_run += rs;
-  };
-  auto prio_m = [&]() {
-    if constexpr (PM == 2) __builtin_amdgcn_s_setprio(1);
-  };
-  auto prio_v = [&]() {
-    if constexpr (PM == 2) __builtin_amdgcn_s_setprio(0);
-  };
-
-  // segment boundary: every LDS read of this wave retired, then the barrier
-  // (a compiler-opaque one: no load is hoisted above it)
-  auto bar = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  // prologue: tile 0 everywhere
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (half == 0) {
-    // global segment 2t: M(t) (+ stage tile t+1); 2t+1: V(t), then tile t+1 landed
-    auto step = [&](auto sc, auto sp, auto sn, int t) {
-      if (t + 1 < nt) stage(decltype(sn)::value, t + 1);
-      prio_m();
-      if (t > 0) pv(sp);
-      qk(sc);
-      prio_v();
-      bar();
-      soft(sc, t);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      bar();
-    };
-    for (int t = 0; t < nt; t += 3) {
-      step(I0{}, I2{}, I1{}, t);
-      if (t + 1 >= nt) break;
-      step(I1{}, I0{}, I2{}, t + 1);
-      if (t + 2 >= nt) break;
-      step(I2{}, I1{}, I0{}, t + 2);
-    }
-    // segment 2nt: P.V of the last tile; 2nt+1: balance the other half's lag
-    prio_m();
-    switch ((nt - 1) % 3) {
-      case 0: pv(I0{}); break;
-      case 1: pv(I1{}); break;
-      default: pv(I2{}); break;
-    }
-    prio_v();
-    bar();
-    bar();
-  } else {
-    // one segment behind: global segment 2t+1: M(t), then tile t+1 landed;
-    // 2t+2: V(t) (+ stage tile t+2).  Segment 0 stages tile 1.
-    if (nt > 1) stage(1, 1);
-    bar();
-    auto step = [&](auto sc, auto sp, auto sf, int t) {
-      prio_m();
-      if (t > 0) pv(sp);
-      qk(sc);
-      prio_v();
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      bar();
-      if (t + 2 < nt) stage(decltype(sf)::value, t + 2);
-      soft(sc, t);
-      bar();
-    };
-    for (int t = 0; t < nt; t += 3) {
-      step(I0{}, I2{}, I2{}, t);
-      if (t + 1 >= nt) break;
-      step(I1{}, I0{}, I0{}, t + 1);
-      if (t + 2 >= nt) break;
-      step(I2{}, I1{}, I1{}, t + 2);
-    }
-    prio_m();
-    switch ((nt - 1) % 3) {
-      case 0: pv(I0{}); break;
-      case 1: pv(I1{}); break;
-      default: pv(I2{}); break;
-    }
-    prio_v();
-    bar();
-  }
-
-  // ---- epilogue: normalise, O[q][d] bf16
-  {
-    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run), __float_as_uint(l_run), false, false);
-    l_run = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
-  }
-  const float inv = 1.f / l_run;
-  if (qrow < a.nq) {
-    bf16_t* op = a.o + ((int64_t)b * a.obs + qrow) * a.ldo + h * D;
-#pragma unroll
-    for (int db = 0; db < NDB; ++db)
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        uint2 pk;
-        pk.x = pack_bf2(o[db][4 * gq] * inv, o[db][4 * gq + 1] * inv);
-        pk.y = pack_bf2(o[db][4 * gq + 2] * inv, o[db][4 * gq + 3] * inv);
-        *(uint2*)(op + db * 32 + 8 * gq + 4 * hl) = pk;
-      }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // D = 64 forward on v_mfma_f32_16x16x32_bf16 (variant 161 = 33 | 128).
 //  * Matrix-core shape: per wave 32 query rows = two 16-query blocks qb, per
 //    64-key tile four 16-key blocks kb; S^T[kb][qb] = K_kb . Q_qb^T leaves
@@ -1147,13 +834,6 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
   if (use16) {
     if (nw == 8) attn16_fwd_kernel<8><<<nwg, 512, 0, s>>>(a);
     else attn16_fwd_kernel<4><<<nwg, 256, 0, s>>>(a);
-    HIP_LAUNCH_CHECK();
-    return VGGT_OK;
-  }
-  if (g_vggt_attn_variant >= 289 && g_vggt_attn_variant <= 291 && a.lse == nullptr && D == 64 && nw == 8) {
-    if (g_vggt_attn_variant == 289) attn_stag_kernel<0><<<nwg, 512, 0, s>>>(a);
-    else if (g_vggt_attn_variant == 290) attn_stag_kernel<1><<<nwg, 512, 0, s>>>(a);
-    else attn_stag_kernel<2><<<nwg, 512, 0, s>>>(a);
     HIP_LAUNCH_CHECK();
     return VGGT_OK;
   }

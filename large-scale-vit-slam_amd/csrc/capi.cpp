@@ -40,10 +40,9 @@ extern "C" int vggt_tune(int knob, int value) {
       return prev;
     case VGGT_TUNE_ATTN_VARIANT:
       // 0-15: bit combinations of the max-tracking kernel; 19/23: pipelined QK^T;
-      // 32/33 (+64 exact scores): offset-free softmax; 161 = 33 on the 16x16x32 MFMA shape (D = 64);
-      // 289-291: 33 with the two wave halves staggered by one segment (D = 64, 8 waves; priority mode 0-2)
+      // 32/33 (+64 exact scores): offset-free softmax; 161 = 33 on the 16x16x32 MFMA shape (D = 64)
       if (value < 0 || (value > 15 && value != 19 && value != 23 && value != 32 && value != 33 && value != 96 &&
-                        value != 97 && value != 161 && (value < 289 || value > 291)))
+                        value != 97 && value != 161))
         return VGGT_ERR_UNSUPPORTED;
       prev = g_vggt_attn_variant;
       g_vggt_attn_variant = value;

@@ -332,70 +332,6 @@ def test_attention_online_softmax_rescale(N, variant):
         N.tune(N.TUNE_ATTN_VARIANT, prev)
 
 
-def _stag_inputs(n, nk, H, case):
-    D = 64
-    C = H * D
-    g = torch.Generator().manual_seed(n + nk)
-    q = torch.randn(n, C, generator=g) * 0.6
-    k = torch.randn(nk, C, generator=g) * 0.6
-    v = torch.randn(nk, C, generator=g)
-    if case == "overflow_late":
-        q[:40] = 4.0
-        k[nk - 50] = 4.0
-    elif case == "all_negative":
-        q[:64] = 4.0
-        k[:] = -3.5 + 0.05 * torch.randn(nk, C, generator=g)
-    elif case == "huge_first_tile":
-        q[:64] = 4.0
-        k[3] = 4.0
-    elif case == "mixed_rows":
-        q[0:128:2] = 4.0
-        q[n - 256:n - 128:2] = 4.0
-        k[10] = 4.0
-        k[nk - 100] = 4.5
-    return q.to(torch.bfloat16).cuda(), k.to(torch.bfloat16).cuda(), v.to(torch.bfloat16).cuda()
-
-
-@pytest.mark.parametrize("variant", [289, 290, 291])
-@pytest.mark.parametrize("n,nk,H,case", [(4100, 4100, 2, "rand"), (5000, 5000, 2, "rand"), (8191, 8191, 2, "rand"),
-                                          (4100, 1, 2, "rand"), (4100, 64, 2, "rand"), (4100, 65, 2, "rand"),
-                                          (4100, 130, 2, "rand"), (4100, 200, 2, "rand"),
-                                          (4200, 4200, 2, "overflow_late"), (4200, 4200, 2, "all_negative"),
-                                          (4200, 4200, 2, "huge_first_tile"), (4200, 4200, 2, "mixed_rows"),
-                                          (16 * 1374, 16 * 1374, 16, "rand")])
-def test_attention_staggered_equals_lockstep(N, variant, n, nk, H, case):
-    """The staggered 8-wave schedule (variants 289-291: waves 4-7 one segment
-    behind waves 0-3, P.V of tile t-1 + QK^T of tile t, then the softmax of
-    tile t; three K|V slots) is variant 33's arithmetic step for step: its
-    output must equal the lockstep 8-wave form bit for bit -- on 1, 2, 3 and
-    4+ KV tiles, every tile count mod 3, ragged last tiles, every branch of the
-    offset-free range guard, and the full global-attention shape."""
-    D = 64
-    C = H * D
-    q, k, v = _stag_inputs(n, nk, H, case)
-    outs = {}
-    prev_w = N.tune(N.TUNE_ATTN_WAVES, 8)
-    try:
-        for var in (33, variant):
-            prev = N.tune(N.TUNE_ATTN_VARIANT, var)
-            try:
-                o = torch.full((n, C), float("nan"), device="cuda", dtype=torch.bfloat16)
-                N.attention(q, k, v, o, 1, H, n, nk, D, n, nk, n)
-                torch.cuda.synchronize()
-                outs[var] = o
-            finally:
-                N.tune(N.TUNE_ATTN_VARIANT, prev)
-    finally:
-        N.tune(N.TUNE_ATTN_WAVES, prev_w)
-    assert torch.isfinite(outs[variant].float()).all()
-    assert torch.equal(outs[variant], outs[33])
-    if n * nk <= 4200 * 4200:
-        t = _ref_attn(q.double().cpu().view(n, H, D).transpose(0, 1), k.double().cpu().view(nk, H, D).transpose(0, 1),
-                      v.double().cpu().view(nk, H, D).transpose(0, 1), D ** -0.5)
-        ref = t.transpose(0, 1).reshape(n, C)
-        assert _rel(outs[variant], ref) < 5e-3, _rel(outs[variant], ref)
-
-
 @pytest.mark.parametrize("variant", [32, 33, 96, 97, 161])
 @pytest.mark.parametrize("case", ["overflow_late", "all_negative", "huge_first_tile", "mixed_rows"])
 @pytest.mark.parametrize("waves,n", [(4, 700), (8, 4200)])
