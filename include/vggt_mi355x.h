@@ -66,6 +66,14 @@ const char* vggt_version(void);
    one compiled; vggt_tune(6, ...) returns VGGT_ERR_UNSUPPORTED) */
 int vggt_tune(int knob, int value);
 
+/* Register the number of CUs launches on `stream` may occupy (a stream created with
+ * hipExtStreamCreateWithCUMask): the persistent kernels size their grid -- one
+ * workgroup per CU -- and their tile-rounding heuristics to it.  cus = 0 forgets the
+ * stream.  Returns the previous count (0 if none), or VGGT_ERR_* (up to 16 streams).
+ * Host-side only; no GPU call.  No reference counterpart: the MI355X multi-GPU
+ * pipeline's encode stream (aligned_vggt/dist/pipeline.py, reserve_cus). */
+int vggt_set_stream_cu_count(void* stream, int cus);
+
 /*
  * out[M,N] = epi( A[M,K] . W[N,K]^T + bias[N] ), bf16 MFMA (v_mfma_f32_16x16x32_bf16),
  * fp32 accumulation.  Replaces every autocast nn.Linear on the bf16 tier:

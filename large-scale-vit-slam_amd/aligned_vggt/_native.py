@@ -29,6 +29,7 @@ _ERR = {VGGT_ERR_SHAPE: "unsupported or inconsistent shape", VGGT_ERR_ALIGN: "mi
 _vp, _i, _i64, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
 _SIGS = {
     "vggt_tune": [_i, _i],
+    "vggt_set_stream_cu_count": [_vp, _i],
     "vggt_gemm_bf16": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _vp, _i64, _vp, _vp, _i64, _vp],
     "vggt_gemm_qkv": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _vp, _i64, _vp, _vp, _vp, _vp, _f, _i, _vp, _i, _vp,
                       _vp, _i, _vp],
@@ -146,6 +147,15 @@ def tune(knob: int, value: int) -> int:
     rc = lib().vggt_tune(knob, value)
     if rc == VGGT_ERR_UNSUPPORTED:
         raise ValueError(f"vggt_tune: unsupported knob/value ({knob}, {value})")
+    return rc
+
+
+def set_stream_cu_count(stream: int, cus: int) -> int:
+    """vggt_set_stream_cu_count: the CUs launches on a CU-masked stream (raw handle) may use;
+    the persistent kernels size their one-workgroup-per-CU grids to it.  0 forgets the stream."""
+    rc = lib().vggt_set_stream_cu_count(ctypes.c_void_p(stream), cus)
+    if rc < 0:
+        raise ValueError(f"vggt_set_stream_cu_count: rejected ({rc})")
     return rc
 
 

@@ -290,11 +290,16 @@ class ChunkPipeline:
         if self.world == 1 and not self.overlap_align:
             mine = self._run_local(images, chunks, num_overlap, keys, memory_shape, B)
         elif self.reserve_cus > 0 and self.device is not None and torch.device(self.device).type == "cuda":
-            enc_stream = self.__dict__.get("_enc_stream")
+            streams = self.__dict__.setdefault("_enc_streams", {})
+            enc_stream = streams.get(self.reserve_cus)
             if enc_stream is None:
+                from .. import _native as N
                 from ..runtime import cu_masked_stream, spread_cus
                 ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
-                enc_stream = self._enc_stream = cu_masked_stream(self.device, spread_cus(ncu, self.reserve_cus))
+                excl = spread_cus(ncu, self.reserve_cus)
+                enc_stream = streams[self.reserve_cus] = cu_masked_stream(self.device, excl)
+                # persistent kernels launched on it size their grids to the CUs it can use
+                N.set_stream_cu_count(enc_stream.cuda_stream, ncu - len(excl))
             cur = torch.cuda.current_stream(self.device)
             enc_stream.wait_stream(cur)
             with torch.cuda.stream(enc_stream):

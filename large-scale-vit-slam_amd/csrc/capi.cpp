@@ -5,6 +5,9 @@ extern "C" const char* vggt_version(void) { return "vggt_mi355x 0.1 gfx950"; }
 
 #include <stdlib.h>
 
+#include <atomic>
+#include <mutex>
+
 #include "tune.h"
 
 namespace {
@@ -59,4 +62,41 @@ extern "C" int vggt_tune(int knob, int value) {
       return prev;
     default: return VGGT_ERR_UNSUPPORTED;
   }
+}
+
+// Streams created with a CU mask and the CUs their launches may use (a handful:
+// the multi-GPU pipeline's encode stream).  Written under a lock, read lock-free.
+namespace {
+constexpr int kMaxMasked = 16;
+std::atomic<void*> g_masked_stream[kMaxMasked];
+std::atomic<int> g_masked_cus[kMaxMasked];
+std::mutex g_masked_mu;
+}  // namespace
+
+int vggt_stream_cu_count(void* stream) {
+  if (!stream) return 0;
+  for (int i = 0; i < kMaxMasked; ++i)
+    if (g_masked_stream[i].load(std::memory_order_acquire) == stream) return g_masked_cus[i].load(std::memory_order_relaxed);
+  return 0;
+}
+
+extern "C" int vggt_set_stream_cu_count(void* stream, int cus) {
+  if (!stream || cus < 0) return VGGT_ERR_SHAPE;
+  std::lock_guard<std::mutex> lk(g_masked_mu);
+  int free_slot = -1;
+  for (int i = 0; i < kMaxMasked; ++i) {
+    void* st = g_masked_stream[i].load(std::memory_order_relaxed);
+    if (st == stream) {
+      const int prev = g_masked_cus[i].load(std::memory_order_relaxed);
+      g_masked_cus[i].store(cus, std::memory_order_relaxed);
+      if (cus == 0) g_masked_stream[i].store(nullptr, std::memory_order_release);
+      return prev;
+    }
+    if (!st && free_slot < 0) free_slot = i;
+  }
+  if (cus == 0) return 0;
+  if (free_slot < 0) return VGGT_ERR_UNSUPPORTED;
+  g_masked_cus[free_slot].store(cus, std::memory_order_relaxed);
+  g_masked_stream[free_slot].store(stream, std::memory_order_release);
+  return 0;
 }

@@ -1554,19 +1554,27 @@ inline int cu_count() {
   }();
   return cus;
 }
+// CUs a launch on stream s can occupy: fewer than the device's for a stream
+// created with a CU mask (vggt_set_stream_cu_count) -- a persistent grid of
+// one workgroup per CU would otherwise leave the masked-off CUs' share for a
+// second, almost empty round
+inline int cu_count(hipStream_t s) {
+  const int n = vggt_stream_cu_count(s);
+  return n > 0 ? n : cu_count();
+}
 
 // Row tile of the persistent form: 256, or 192 when whole rounds of 192-row
 // tiles over the CUs cost at least 10% less (the N = 1024 projections at
 // M = 21,984: 344 tiles = 1.34 rounds at 256 rows, 460 = 1.80 at 192); the
 // residual epilogue always uses 192 rows (register budget: rx + acc)
-inline int ppp_pick_bm(int epi, int M, int N) {
+inline int ppp_pick_bm(int epi, int M, int N, hipStream_t s) {
   if (epi == VGGT_EPI_RESID_F32) return 192;
   static int force = [] {  // VGGT_GEMM_BM=192/256: A/B override
     const char* e = getenv("VGGT_GEMM_BM");
     return e ? atoi(e) : 0;
   }();
   if (force == 192 || force == 256) return force;
-  const int cus = cu_count();
+  const int cus = cu_count(s);
   const long r256 = ((long)((M + 255) / 256) * (N / 256) + cus - 1) / cus;
   const long r192 = ((long)((M + 191) / 192) * (N / 256) + cus - 1) / cus;
   return r192 * 192 * 10 < r256 * 256 * 9 ? 192 : 256;
@@ -1584,7 +1592,8 @@ int launch_ppp_fk(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, in
   const int lds = ppp_lds_bytes(EPI, BMT, N, ep);
   if (!lds) return VGGT_ERR_SHAPE;
   const int ntiles = ((M + BMT - 1) / BMT) * (N / 256);
-  const int nwg = ntiles < cu_count() ? ntiles : cu_count();
+  const int cus = cu_count(s);
+  const int nwg = ntiles < cus ? ntiles : cus;
   // M-tiles per tile group (VGGT_GEMM_GM overrides; 0 = row-major).  Aggregator
   // step 98.45 -> 97.3-97.6 ms at 4 (8: 97.55, 16: 98.5); fc1 at K = 4096 625 ->
   // 591 us (r3y, r3z)
@@ -1623,7 +1632,7 @@ int launch_ppp(const bf16_t* a, int64_t lda, const bf16_t* w, int64_t ldw, int M
     // 128x128 form, aggregator step 104.9 vs 101.3 ms, r3r)
     return launch_ppp_bm<EPI, 192>(a, lda, w, ldw, M, N, K, ep, s);
   } else {
-    if (ppp_pick_bm(EPI, M, N) == 192) return launch_ppp_bm<EPI, 192>(a, lda, w, ldw, M, N, K, ep, s);
+    if (ppp_pick_bm(EPI, M, N, s) == 192) return launch_ppp_bm<EPI, 192>(a, lda, w, ldw, M, N, K, ep, s);
     return launch_ppp_bm<EPI, 256>(a, lda, w, ldw, M, N, K, ep, s);
   }
 }
@@ -1853,7 +1862,7 @@ extern "C" int vggt_gemm_qkv(const void* A, int64_t lda, const void* W, int64_t 
   if (g_vggt_gemm_tile < 0 && mode == 7 && M >= 4096 && (persist_policy() & 2)) mode = 9;
   if (mode == 9) {
     bool ok = D == 64 && N % 256 == 0 && N <= PP_MAXN && K % PBK == 0 && rope_mode != VGGT_ROPE_1D &&
-              (int64_t)PBM * ldo * 2 < (1ll << 31) && ppp_lds_bytes(EPI_QKNORM_D64, ppp_pick_bm(EPI_QKNORM_D64, M, N), N, ep) > 0;
+              (int64_t)PBM * ldo * 2 < (1ll << 31) && ppp_lds_bytes(EPI_QKNORM_D64, ppp_pick_bm(EPI_QKNORM_D64, M, N, s), N, ep) > 0;
     if (ok && rope_mode == VGGT_ROPE_2D) {
       // positions are staged as bytes; tables of at most 256 positions
       ok = tab_len <= 256;

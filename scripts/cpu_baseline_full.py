@@ -15,7 +15,8 @@ SURVEY.md §8c).  Writes one JSON (default profiles/cpu_baseline_full.json),
 which bench.py attaches to its cpu_baseline.
 
   python scripts/cpu_baseline_full.py [--rows C1,C2] [--threads 16,0] [--runs 3] [--out PATH] [--append]
-      (--threads 0 = os.cpu_count())
+      (--threads 0 = os.cpu_count(); --append adds this call's timed runs to a row's earlier ones, so a
+      slow row can be measured over several bounded calls -- each call still does its own warm-up)
 """
 from __future__ import annotations
 
@@ -122,11 +123,13 @@ def main():
                     full()
                     ts.append(time.perf_counter() - t0)
                     print(f"[{time.strftime('%H:%M:%S')}] {row} threads={th} run {i}: {ts[-1]:.1f} s", flush=True)
-            med = statistics.median(ts)
-            res["rows"][f"{row}_t{th}"] = {"row": row, "workload": what, "threads": th, "runs": a.runs,
-                                           "warmup_s": round(tw, 2),
-                                           "runs_s": [round(x, 2) for x in ts], "median_s_per_chunk": round(med, 2),
-                                           "chunks_per_s": round(1.0 / med, 6)}
+            key = f"{row}_t{th}"
+            prev = res["rows"].get(key, {}).get("runs_s", []) if a.append else []
+            allr = prev + [round(x, 2) for x in ts]  # --append: runs of earlier calls (one GPU-box lease each) kept
+            med = statistics.median(allr)
+            res["rows"][key] = {"row": row, "workload": what, "threads": th, "runs": len(allr),
+                                "warmup_s": round(tw, 2), "runs_s": allr, "median_s_per_chunk": round(med, 2),
+                                "chunks_per_s": round(1.0 / med, 6)}
             with open(a.out, "w") as f:  # after every row: a killed run keeps what it measured
                 json.dump(res, f, indent=1)
     state["done"] = True

@@ -69,3 +69,20 @@ def test_tune_knobs_range_and_restore():
     if "VGGT_ATTN16" not in os.environ:
         p = lib.vggt_tune(N.TUNE_ATTN16, 2)
         assert p == 2
+
+
+def test_stream_cu_count_registry():
+    """vggt_set_stream_cu_count (host-side table, no GPU call): returns the previous
+    count, 0 forgets the stream, a null stream or negative count is rejected."""
+    from aligned_vggt import _native as N
+    if not os.path.exists(N.LIB_PATH):
+        pytest.skip("library not built")
+    fake = 0x1234560  # never dereferenced: the table only compares handles
+    assert N.set_stream_cu_count(fake, 240) == 0
+    assert N.set_stream_cu_count(fake, 224) == 240
+    assert N.set_stream_cu_count(fake, 0) == 224
+    assert N.set_stream_cu_count(fake, 0) == 0
+    with pytest.raises(ValueError):
+        N.set_stream_cu_count(0, 8)
+    with pytest.raises(ValueError):
+        N.set_stream_cu_count(fake, -1)

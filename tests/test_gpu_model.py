@@ -75,21 +75,21 @@ def test_feature_aligned_two_chunks(models, S, ov, H, W):
     print("hip vs bf16 emulation", e_hip)
     print("hip vs fp32", e_hip32)
     print("ref bf16 vs fp32", e_ref)
-    # North-star tolerance on the Sim(3) alignment outputs: 1e-3 relative.
-    assert e_hip["chunk_sim3"] < 1e-3, e_hip
-    # Everything else: within 3e-2 of the bf16 emulation, or -- where random-init
-    # camera / decoder weights amplify token-level rounding chaotically -- no
-    # further from the fp32 numerics than twice the reference's own bf16 run.
-    # pose_enc with overlap > 1 goes through the Markley eigen-average of the
-    # overlap transforms (geometry.py:4-37), which amplifies that rounding
-    # further: the reference's own bf16-vs-fp32 spread on the (4, 2) case varies
-    # 0.025-0.066 between runs of the CPU oracle itself, so there the bar is the
-    # fp32 distance within 3x that spread or 6e-2 of the bf16 emulation.
+    # Per-output bars vs the bf16-mixed emulation, about 2x the values measured on
+    # MI355X (round 4: chunk_sim3 6.3e-4 / 6.1e-4, frame_se3 9.1e-4 / 9.4e-4, depth
+    # 4.2e-4 / 2.9e-4, depth_conf 1.1e-5, overlap tokens 7.6e-3, memory 3.0e-3 /
+    # 3.5e-3, points 1.3e-2 / 1.9e-2, pose_enc 1.6e-2 / 3.7e-2 for (3, 1) / (4, 2)),
+    # the chunk Sim(3) at the north star's 1e-3.  Points and poses pass through
+    # random-init camera / decoder weights that amplify token-level rounding (and,
+    # at overlap 2, the Markley eigen-average of geometry.py:4-37), so they are
+    # ALSO held to their distance from the fp32 numerics: within 2x (poses) /
+    # 1.5x (points) of the reference's own bf16-vs-fp32 spread.
+    bars = {"chunk_sim3": 1e-3, "frame_se3": 2e-3, "depth": 1.5e-3, "depth_conf": 5e-5, "overlap_tokens": 1.2e-2,
+            "memory": 6e-3, "points": 3e-2, "pose_enc": 5e-2 if ov > 1 else 3e-2}
     for k, v in e_hip.items():
-        if k == "pose_enc" and ov > 1:
-            assert v < 6e-2 or e_hip32[k] < 3.0 * e_ref[k], (k, e_hip, e_hip32, e_ref)
-        else:
-            assert v < 3e-2 or e_hip32[k] < 2.0 * e_ref[k], (k, e_hip, e_hip32, e_ref)
+        assert v < bars[k], (k, v, bars[k], e_hip)
+    assert e_hip32["pose_enc"] < 2.0 * e_ref["pose_enc"], (e_hip32, e_ref)
+    assert e_hip32["points"] < 1.5 * e_ref["points"], (e_hip32, e_ref)
 
 
 def test_heads_fp32_tier_tight(models):
