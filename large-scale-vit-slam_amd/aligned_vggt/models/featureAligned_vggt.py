@@ -35,13 +35,15 @@ from ..utils.pose_enc import extri_intri_to_pose_encoding, pose_encoding_to_extr
 # (~300 small launches per chunk, profiles/r4w).  Training always takes the
 # differentiable torch form.
 _POSE_MODE = os.environ.get("VGGT_POSE", "hip")
-# no-grad inference: the recurrent part of align_chunk (alignment head from its first
-# temporal block on, decoder, GatedUpdate, pose composition: ~300 launches, most of
-# them microseconds long) replays as ONE HIP graph per shape (_AlignGraph), and the
-# head's context-free prefix (project_in, token_norm, frame block 0) runs in
-# encode_chunk, off the recurrence.  VGGT_ALIGN_GRAPH=0: eager launches;
-# VGGT_ALIGN_PREFIX=0: the whole head in align_chunk.
-_ALIGN_GRAPH = os.environ.get("VGGT_ALIGN_GRAPH", "1") != "0"
+# no-grad inference: the head's context-free prefix (project_in, token_norm, frame
+# block 0) runs in encode_chunk, off the recurrence (VGGT_ALIGN_PREFIX=0: the whole
+# head in align_chunk).  VGGT_ALIGN_GRAPH=1 replays the recurrent part (alignment head
+# from its first temporal block on, decoder, GatedUpdate, pose composition: ~300
+# launches) as ONE HIP graph per shape (_AlignGraph) -- off by default: measured no
+# faster alone (2.45-2.77 ms eager vs 2.47-2.52 ms per 154x518 chunk) and much slower
+# beside a concurrent encode (7.6 vs 13.2 ms; the graph's kernels do not win the CUs
+# the way the high-priority stream's own launches do), profiles/r8.
+_ALIGN_GRAPH = os.environ.get("VGGT_ALIGN_GRAPH", "0") == "1"
 _ALIGN_PREFIX = os.environ.get("VGGT_ALIGN_PREFIX", "1") != "0"
 
 try:  # optional, as in the reference (featureAligned_vggt.py:3); only used for from_pretrained

@@ -88,11 +88,11 @@ def test_overlapped_schedule_matches_sequential_loop(cuda, monkeypatch, group, r
 
 @pytest.mark.parametrize("H,W,w,ov,nm", [(56, 70, 8, 2, 8), (42, 56, 5, 1, 0)])
 def test_graphed_prefix_align_matches_eager(cuda, monkeypatch, H, W, w, ov, nm):
-    """align_chunk's default inference path -- the alignment head's context-free
-    prefix (project_in, token_norm, frame block 0) run in encode_chunk and the
-    recurrent rest replayed from one HIP graph per shape -- against the eager
-    whole-head path (VGGT_ALIGN_GRAPH=0, VGGT_ALIGN_PREFIX=0) over a sequence
-    with a shorter tail chunk (two graph shapes) and repeated graph replays."""
+    """align_chunk's inference paths -- the alignment head's context-free prefix
+    (project_in, token_norm, frame block 0) run in encode_chunk (default), and with
+    it the recurrent rest replayed from one HIP graph per shape (VGGT_ALIGN_GRAPH=1)
+    -- against the eager whole-head path (VGGT_ALIGN_PREFIX=0) over a sequence with
+    a shorter tail chunk (two graph shapes) and repeated graph replays."""
     from aligned_vggt.dist.pipeline import apply_sequence_to_model
     from aligned_vggt.models import featureAligned_vggt as FAmod
     from aligned_vggt.utils.synthetic import synthetic_images
