@@ -66,13 +66,20 @@ const char* vggt_version(void);
    one compiled; vggt_tune(6, ...) returns VGGT_ERR_UNSUPPORTED) */
 int vggt_tune(int knob, int value);
 
-/* Register the number of CUs launches on `stream` may occupy (a stream created with
- * hipExtStreamCreateWithCUMask): the persistent kernels size their grid -- one
- * workgroup per CU -- and their tile-rounding heuristics to it.  cus = 0 forgets the
- * stream.  Returns the previous count (0 if none), or VGGT_ERR_* (up to 16 streams).
- * Host-side only; no GPU call.  No reference counterpart: the MI355X multi-GPU
- * pipeline's encode stream (aligned_vggt/dist/pipeline.py, reserve_cus). */
-int vggt_set_stream_cu_count(void* stream, int cus);
+/* Per-stream launch configuration, host-side only (no GPU call); no reference
+ * counterpart: the MI355X multi-GPU pipeline's encode stream (aligned_vggt/dist/pipeline.py).
+ *   cus    the CUs launches on `stream` may occupy (a stream created with
+ *          hipExtStreamCreateWithCUMask; 0 = the device's): the persistent kernels size
+ *          their one-workgroup-per-CU grids and tile-rounding heuristics to it;
+ *   flags  VGGT_STREAM_SHORT_WORKGROUPS: no persistent GEMM forms on this stream -- every
+ *          workgroup runs one output tile, so kernels of a concurrent high-priority stream
+ *          (the alignment recurrence) find free CUs within microseconds instead of
+ *          waiting for a whole persistent launch.  Results are unchanged up to fp32
+ *          summation order inside a tile.
+ * cus = flags = 0 forgets the stream.  Returns the previous setting (cus | flags << 16,
+ * 0 if none), or VGGT_ERR_* (up to 16 streams). */
+#define VGGT_STREAM_SHORT_WORKGROUPS 1
+int vggt_set_stream_config(void* stream, int cus, int flags);
 
 /*
  * out[M,N] = epi( A[M,K] . W[N,K]^T + bias[N] ), bf16 MFMA (v_mfma_f32_16x16x32_bf16),

@@ -29,7 +29,7 @@ _ERR = {VGGT_ERR_SHAPE: "unsupported or inconsistent shape", VGGT_ERR_ALIGN: "mi
 _vp, _i, _i64, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
 _SIGS = {
     "vggt_tune": [_i, _i],
-    "vggt_set_stream_cu_count": [_vp, _i],
+    "vggt_set_stream_config": [_vp, _i, _i],
     "vggt_gemm_bf16": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _vp, _i64, _vp, _vp, _i64, _vp],
     "vggt_gemm_qkv": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _vp, _i64, _vp, _vp, _vp, _vp, _f, _i, _vp, _i, _vp,
                       _vp, _i, _vp],
@@ -150,12 +150,16 @@ def tune(knob: int, value: int) -> int:
     return rc
 
 
-def set_stream_cu_count(stream: int, cus: int) -> int:
-    """vggt_set_stream_cu_count: the CUs launches on a CU-masked stream (raw handle) may use;
-    the persistent kernels size their one-workgroup-per-CU grids to it.  0 forgets the stream."""
-    rc = lib().vggt_set_stream_cu_count(ctypes.c_void_p(stream), cus)
+STREAM_SHORT_WORKGROUPS = 1
+
+
+def set_stream_config(stream: int, cus: int, flags: int = 0) -> int:
+    """vggt_set_stream_config on a raw stream handle: the CUs its launches may use (a CU-masked
+    stream; 0 = the device's) and STREAM_* flags.  Returns the previous cus | flags << 16;
+    cus = flags = 0 forgets the stream."""
+    rc = lib().vggt_set_stream_config(ctypes.c_void_p(stream), cus, flags)
     if rc < 0:
-        raise ValueError(f"vggt_set_stream_cu_count: rejected ({rc})")
+        raise ValueError(f"vggt_set_stream_config: rejected ({rc})")
     return rc
 
 

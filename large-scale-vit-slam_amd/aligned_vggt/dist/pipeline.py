@@ -173,6 +173,14 @@ class ChunkPipeline:
         # over the XCDs), so the alignment recurrence's kernels never queue behind a
         # full-chip encode launch; VGGT_ALIGN_RESERVE_CUS sets the default (0: off)
         self.reserve_cus = int(os.environ.get("VGGT_ALIGN_RESERVE_CUS", "0"))
+        # short_workgroups: in the ring's schedule the encodes run on a dedicated
+        # stream configured for short workgroups (vggt_set_stream_config: no
+        # persistent GEMM forms, whose one-workgroup-per-CU grids hold every CU for a
+        # whole launch), so the alignment's kernels on the high-priority stream find
+        # CUs within microseconds: t_align beside an encode 7.6 -> 5.1 ms per 154x518
+        # chunk for +10 % encode time, the 8-rank bound 43 t_align / (T1/8) 2.1 -> 1.3
+        # (DESIGN.md §8c).  VGGT_RING_SHORT_WG=0 turns it off.
+        self.short_workgroups = os.environ.get("VGGT_RING_SHORT_WG", "1") != "0"
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -289,17 +297,9 @@ class ChunkPipeline:
         self.align_events = []
         if self.world == 1 and not self.overlap_align:
             mine = self._run_local(images, chunks, num_overlap, keys, memory_shape, B)
-        elif self.reserve_cus > 0 and self.device is not None and torch.device(self.device).type == "cuda":
-            streams = self.__dict__.setdefault("_enc_streams", {})
-            enc_stream = streams.get(self.reserve_cus)
-            if enc_stream is None:
-                from .. import _native as N
-                from ..runtime import cu_masked_stream, spread_cus
-                ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
-                excl = spread_cus(ncu, self.reserve_cus)
-                enc_stream = streams[self.reserve_cus] = cu_masked_stream(self.device, excl)
-                # persistent kernels launched on it size their grids to the CUs it can use
-                N.set_stream_cu_count(enc_stream.cuda_stream, ncu - len(excl))
+        elif ((self.reserve_cus > 0 or self.short_workgroups) and self.device is not None
+              and torch.device(self.device).type == "cuda"):
+            enc_stream = self._encode_stream()
             cur = torch.cuda.current_stream(self.device)
             enc_stream.wait_stream(cur)
             with torch.cuda.stream(enc_stream):
@@ -310,6 +310,30 @@ class ChunkPipeline:
         else:
             mine = self._run_ring(images, chunks, num_overlap, keys, token_dims, memory_shape, B)
         return self._gather(mine, chunks, num_overlap, B)
+
+    def _encode_stream(self):
+        """The ring's encode stream (cached per configuration): a dedicated
+        non-blocking HIP stream, or one masked off `reserve_cus` CUs, registered
+        with the library (vggt_set_stream_config) so its persistent kernels size
+        their grids to the CUs it can use and, with short_workgroups, it gets no
+        persistent GEMM forms at all."""
+        from .. import _native as N
+        from ..runtime import cu_masked_stream, dedicated_stream, spread_cus
+        key = (self.reserve_cus, self.short_workgroups)
+        streams = self.__dict__.setdefault("_enc_streams", {})
+        s = streams.get(key)
+        if s is None:
+            cus = 0
+            if self.reserve_cus > 0:
+                ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+                excl = spread_cus(ncu, self.reserve_cus)
+                s = cu_masked_stream(self.device, excl)
+                cus = ncu - len(excl)
+            else:
+                s = dedicated_stream(self.device)
+            N.set_stream_config(s.cuda_stream, cus, N.STREAM_SHORT_WORKGROUPS if self.short_workgroups else 0)
+            streams[key] = s
+        return s
 
     def _groups(self, chunks, own: List[int], images) -> List[List[int]]:
         """Encode groups over this rank's own chunks (runs of equal length)."""

@@ -205,12 +205,7 @@ def spread_cus(ncu: int, n: int) -> list:
 _HIP = None
 
 
-def cu_masked_stream(device, exclude) -> "torch.cuda.ExternalStream":
-    """A HIP stream whose kernels never run on the CUs in ``exclude``
-    (hipExtStreamCreateWithCUMask), as a torch ExternalStream.  The multi-GPU
-    pipeline encodes on such a stream so that the alignment recurrence's
-    kernels, on their own high-priority stream, always find those CUs free
-    instead of waiting behind a persistent GEMM or attention launch."""
+def _hip():
     import ctypes
     global _HIP
     if _HIP is None:
@@ -218,6 +213,33 @@ def cu_masked_stream(device, exclude) -> "torch.cuda.ExternalStream":
         _HIP.hipExtStreamCreateWithCUMask.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
                                                       ctypes.POINTER(ctypes.c_uint32)]
         _HIP.hipExtStreamCreateWithCUMask.restype = ctypes.c_int
+        _HIP.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+        _HIP.hipStreamCreateWithFlags.restype = ctypes.c_int
+    return _HIP
+
+
+def dedicated_stream(device) -> "torch.cuda.ExternalStream":
+    """A HIP stream of its own (non-blocking; not one of torch's pooled streams,
+    which other users are handed too), as a torch ExternalStream -- for a
+    per-stream library configuration (vggt_set_stream_config) that must apply to
+    this stream's work only."""
+    import ctypes
+    device = torch.device(device)
+    s = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        rc = _hip().hipStreamCreateWithFlags(ctypes.byref(s), 1)  # hipStreamNonBlocking
+    if rc != 0:
+        raise RuntimeError(f"hipStreamCreateWithFlags failed ({rc})")
+    return torch.cuda.ExternalStream(s.value, device=device)
+
+
+def cu_masked_stream(device, exclude) -> "torch.cuda.ExternalStream":
+    """A HIP stream whose kernels never run on the CUs in ``exclude``
+    (hipExtStreamCreateWithCUMask), as a torch ExternalStream.  The multi-GPU
+    pipeline encodes on such a stream so that the alignment recurrence's
+    kernels, on their own high-priority stream, always find those CUs free
+    instead of waiting behind a persistent GEMM or attention launch."""
+    import ctypes
     device = torch.device(device)
     ncu = torch.cuda.get_device_properties(device).multi_processor_count
     words = [0xFFFFFFFF] * ((ncu + 31) // 32)
@@ -228,7 +250,7 @@ def cu_masked_stream(device, exclude) -> "torch.cuda.ExternalStream":
     arr = (ctypes.c_uint32 * len(words))(*words)
     s = ctypes.c_void_p()
     with torch.cuda.device(device):
-        rc = _HIP.hipExtStreamCreateWithCUMask(ctypes.byref(s), len(words), arr)
+        rc = _hip().hipExtStreamCreateWithCUMask(ctypes.byref(s), len(words), arr)
     if rc != 0:
         raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
     return torch.cuda.ExternalStream(s.value, device=device)

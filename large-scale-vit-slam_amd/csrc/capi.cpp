@@ -64,39 +64,53 @@ extern "C" int vggt_tune(int knob, int value) {
   }
 }
 
-// Streams created with a CU mask and the CUs their launches may use (a handful:
-// the multi-GPU pipeline's encode stream).  Written under a lock, read lock-free.
+// Per-stream launch configuration (a handful of streams: the multi-GPU pipeline's
+// encode streams): the CUs launches may use (CU-masked streams) and flags.
+// Written under a lock, read lock-free.
 namespace {
-constexpr int kMaxMasked = 16;
-std::atomic<void*> g_masked_stream[kMaxMasked];
-std::atomic<int> g_masked_cus[kMaxMasked];
-std::mutex g_masked_mu;
+constexpr int kMaxStreams = 16;
+std::atomic<void*> g_cfg_stream[kMaxStreams];
+std::atomic<int> g_cfg_cus[kMaxStreams];
+std::atomic<int> g_cfg_flags[kMaxStreams];
+std::mutex g_cfg_mu;
+int find_cfg(void* stream) {
+  if (!stream) return -1;
+  for (int i = 0; i < kMaxStreams; ++i)
+    if (g_cfg_stream[i].load(std::memory_order_acquire) == stream) return i;
+  return -1;
+}
 }  // namespace
 
 int vggt_stream_cu_count(void* stream) {
-  if (!stream) return 0;
-  for (int i = 0; i < kMaxMasked; ++i)
-    if (g_masked_stream[i].load(std::memory_order_acquire) == stream) return g_masked_cus[i].load(std::memory_order_relaxed);
-  return 0;
+  const int i = find_cfg(stream);
+  return i < 0 ? 0 : g_cfg_cus[i].load(std::memory_order_relaxed);
 }
 
-extern "C" int vggt_set_stream_cu_count(void* stream, int cus) {
-  if (!stream || cus < 0) return VGGT_ERR_SHAPE;
-  std::lock_guard<std::mutex> lk(g_masked_mu);
-  int free_slot = -1;
-  for (int i = 0; i < kMaxMasked; ++i) {
-    void* st = g_masked_stream[i].load(std::memory_order_relaxed);
-    if (st == stream) {
-      const int prev = g_masked_cus[i].load(std::memory_order_relaxed);
-      g_masked_cus[i].store(cus, std::memory_order_relaxed);
-      if (cus == 0) g_masked_stream[i].store(nullptr, std::memory_order_release);
-      return prev;
-    }
-    if (!st && free_slot < 0) free_slot = i;
+int vggt_stream_flags(void* stream) {
+  const int i = find_cfg(stream);
+  return i < 0 ? 0 : g_cfg_flags[i].load(std::memory_order_relaxed);
+}
+
+extern "C" int vggt_set_stream_config(void* stream, int cus, int flags) {
+  if (!stream || cus < 0 || (flags & ~VGGT_STREAM_SHORT_WORKGROUPS)) return VGGT_ERR_SHAPE;
+  std::lock_guard<std::mutex> lk(g_cfg_mu);
+  int slot = find_cfg(stream);
+  const int prev = slot < 0 ? 0 : (g_cfg_cus[slot].load(std::memory_order_relaxed) |
+                                    g_cfg_flags[slot].load(std::memory_order_relaxed) << 16);
+  if (cus == 0 && flags == 0) {
+    if (slot >= 0) g_cfg_stream[slot].store(nullptr, std::memory_order_release);
+    return prev;
   }
-  if (cus == 0) return 0;
-  if (free_slot < 0) return VGGT_ERR_UNSUPPORTED;
-  g_masked_cus[free_slot].store(cus, std::memory_order_relaxed);
-  g_masked_stream[free_slot].store(stream, std::memory_order_release);
-  return 0;
+  if (slot < 0) {
+    for (int i = 0; i < kMaxStreams && slot < 0; ++i)
+      if (!g_cfg_stream[i].load(std::memory_order_relaxed)) slot = i;
+    if (slot < 0) return VGGT_ERR_UNSUPPORTED;
+    g_cfg_cus[slot].store(cus, std::memory_order_relaxed);
+    g_cfg_flags[slot].store(flags, std::memory_order_relaxed);
+    g_cfg_stream[slot].store(stream, std::memory_order_release);
+  } else {
+    g_cfg_cus[slot].store(cus, std::memory_order_relaxed);
+    g_cfg_flags[slot].store(flags, std::memory_order_relaxed);
+  }
+  return prev;
 }

@@ -1020,12 +1020,13 @@ constexpr int PP_LDS_MAX = 160 * 1024;
 // VGGT_GEMM_PERSIST (A/B of the auto policy): bit 0 = the persistent form for
 // the bf16 / GELU / f32 GEMMs, bit 1 = for the fused qkv GEMM, bit 2 = for the
 // LayerScale-residual GEMMs (default all)
-inline int persist_policy() {
+inline int persist_policy(hipStream_t s) {
   static int p = [] {
     const char* e = getenv("VGGT_GEMM_PERSIST");
     return e ? atoi(e) : 7;
   }();
-  return p;
+  // a stream configured for short workgroups (vggt_set_stream_config) gets none of the persistent forms
+  return (vggt_stream_flags(s) & VGGT_STREAM_SHORT_WORKGROUPS) ? 0 : p;
 }
 
 // sum over the four 16-lane rows of a wave (lanes l, l^16, l^32, l^48)
@@ -1555,7 +1556,7 @@ inline int cu_count() {
   return cus;
 }
 // CUs a launch on stream s can occupy: fewer than the device's for a stream
-// created with a CU mask (vggt_set_stream_cu_count) -- a persistent grid of
+// created with a CU mask (vggt_set_stream_config) -- a persistent grid of
 // one workgroup per CU would otherwise leave the masked-off CUs' share for a
 // second, almost empty round
 inline int cu_count(hipStream_t s) {
@@ -1715,20 +1716,20 @@ int gemm_impl(const void* A, int64_t lda, const void* W, int64_t ldw, const floa
   // (GELU from M = 4,096: the 154x518 sequence chunk's fc1, 6,592 rows: 72.9 -> 64.8 us, r3w; plain bf16 stays on
   // the one-shot forms below 16,384 rows: qkv shape 49-55 vs 55 us)
   if (g_vggt_gemm_tile < 0 && mode == 7 && (M >= 16384 || epi == VGGT_EPI_GELU_BF16) && N <= PP_MAXN &&
-      (persist_policy() & 1))
+      (persist_policy(s) & 1))
     mode = 9;
   // ... and the narrow (N = 1024) bf16 / f32-output GEMMs of the training
   // recompute and backward (dX = dY W): 192-row persistent tiles instead of
   // 128x128 at 22,000 rows: K = 4096 177 -> 144 us, K = 3072 132 -> 112 us,
   // K = 1024 51.5 -> 45.4 us (gemmbench r3tr)
   if (g_vggt_gemm_tile < 0 && mode == 0 && epi != VGGT_EPI_RESID_F32 && M >= 16384 && N % 256 == 0 &&
-      N <= PP_MAXN && K % PBK == 0 && (persist_policy() & 1))
+      N <= PP_MAXN && K % PBK == 0 && (persist_policy(s) & 1))
     mode = 9;
   // the LayerScale-residual fc2 (N = 1024, K = 4096) on 192-row persistent tiles:
   // 216 -> 201 us, aggregator step 104.0 -> 102.3 ms (same box, r3o); the
   // K = 1024 proj stays on the 128x128 form (76 vs 80 us)
   if (g_vggt_gemm_tile < 0 && epi == VGGT_EPI_RESID_F32 && M >= 16384 && N % 256 == 0 && N <= PP_MAXN &&
-      K % PBK == 0 && K >= 2048 && (persist_policy() & 4))
+      K % PBK == 0 && K >= 2048 && (persist_policy(s) & 4))
     mode = 9;
   if (mode >= 3 && mode <= 7 && K % PBK) mode = 2;    // the ping-pong form steps K by 64
   if (mode == 0 && K % BK) mode = 2;     // the 128x128 form steps K by 64
@@ -1859,7 +1860,7 @@ extern "C" int vggt_gemm_qkv(const void* A, int64_t lda, const void* W, int64_t 
   if (mode != 0 && (int64_t)RBM * (lda > ldw ? lda : ldw) * 2 >= (1ll << 31)) return VGGT_ERR_SHAPE;
   // auto: the persistent form on the chunk shapes (D = 64 heads, RoPE-2D or none)
   // (fused qkv of the 154x518 sequence chunk, 6,592 rows: 68.9 -> 53.6 us, r3w)
-  if (g_vggt_gemm_tile < 0 && mode == 7 && M >= 4096 && (persist_policy() & 2)) mode = 9;
+  if (g_vggt_gemm_tile < 0 && mode == 7 && M >= 4096 && (persist_policy(s) & 2)) mode = 9;
   if (mode == 9) {
     bool ok = D == 64 && N % 256 == 0 && N <= PP_MAXN && K % PBK == 0 && rope_mode != VGGT_ROPE_1D &&
               (int64_t)PBM * ldo * 2 < (1ll << 31) && ppp_lds_bytes(EPI_QKNORM_D64, ppp_pick_bm(EPI_QKNORM_D64, M, N, s), N, ep) > 0;

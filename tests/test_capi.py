@@ -71,18 +71,19 @@ def test_tune_knobs_range_and_restore():
         assert p == 2
 
 
-def test_stream_cu_count_registry():
-    """vggt_set_stream_cu_count (host-side table, no GPU call): returns the previous
-    count, 0 forgets the stream, a null stream or negative count is rejected."""
+def test_stream_config_registry():
+    """vggt_set_stream_config (host-side table, no GPU call): returns the previous
+    setting (cus | flags << 16), cus = flags = 0 forgets the stream, a null stream,
+    a negative count or an unknown flag is rejected."""
     from aligned_vggt import _native as N
     if not os.path.exists(N.LIB_PATH):
         pytest.skip("library not built")
     fake = 0x1234560  # never dereferenced: the table only compares handles
-    assert N.set_stream_cu_count(fake, 240) == 0
-    assert N.set_stream_cu_count(fake, 224) == 240
-    assert N.set_stream_cu_count(fake, 0) == 224
-    assert N.set_stream_cu_count(fake, 0) == 0
-    with pytest.raises(ValueError):
-        N.set_stream_cu_count(0, 8)
-    with pytest.raises(ValueError):
-        N.set_stream_cu_count(fake, -1)
+    assert N.set_stream_config(fake, 240) == 0
+    assert N.set_stream_config(fake, 224, N.STREAM_SHORT_WORKGROUPS) == 240
+    assert N.set_stream_config(fake, 0, N.STREAM_SHORT_WORKGROUPS) == 224 | 1 << 16
+    assert N.set_stream_config(fake, 0, 0) == 1 << 16
+    assert N.set_stream_config(fake, 0, 0) == 0
+    for bad in ((0, 8, 0), (fake, -1, 0), (fake, 0, 2)):
+        with pytest.raises(ValueError):
+            N.set_stream_config(*bad)
