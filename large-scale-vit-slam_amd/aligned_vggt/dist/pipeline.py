@@ -159,7 +159,7 @@ class ChunkPipeline:
 
     def __init__(self, model, group=None, device=None, gather_dense: bool = False,
                  encode_group: Optional[int] = None, overlap_align: Optional[bool] = None,
-                 time_align: bool = False):
+                 time_align: bool = False, short_workgroups: Optional[bool] = None):
         self.model = model
         # one rank: align chunk i on the side stream while the next encode group
         # runs (the ring's schedule with the baton kept on the device);
@@ -180,7 +180,9 @@ class ChunkPipeline:
         # CUs within microseconds: t_align beside an encode 7.6 -> 5.1 ms per 154x518
         # chunk for +10 % encode time, the 8-rank bound 43 t_align / (T1/8) 2.1 -> 1.3
         # (DESIGN.md §8c).  VGGT_RING_SHORT_WG=0 turns it off.
-        self.short_workgroups = os.environ.get("VGGT_RING_SHORT_WG", "1") != "0"
+        if short_workgroups is None:
+            short_workgroups = os.environ.get("VGGT_RING_SHORT_WG", "1") != "0"
+        self.short_workgroups = short_workgroups
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
