@@ -243,10 +243,14 @@ int vggt_layernorm_grouped(const void* x, int in_dtype, int64_t ldx, const float
  */
 int vggt_linear_f32(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, int M, int N, int K,
                     int act_in, int epi, float* out, int64_t ldo, const float* gamma, void* stream);
-/* Same with a caller-provided scratch (device, >= 16 * roundup(M,64) * N floats
- * to allow the maximum split): skinny-M calls are split along K into up to 16
- * deterministic partial sums combined in a fixed order (camera head trunk,
- * alignment decoder: M = 16 frames).  ws == NULL: no split. */
+/* Same with a caller-provided scratch (device, >= VGGT_LINEAR_F32_WS_COUNTERS * 4 +
+ * 16 * roundup(M,64) * N * 4 bytes to allow the maximum split): skinny-M calls are
+ * split along K into up to 16 deterministic partial sums combined in a fixed order
+ * (camera head trunk, alignment decoder: M = 16 frames) by the last split block of
+ * each output tile, in the same launch.  The scratch's first
+ * VGGT_LINEAR_F32_WS_COUNTERS words are per-tile counters: zero-fill them before a
+ * scratch's first use; every call leaves them zero.  ws == NULL: no split. */
+#define VGGT_LINEAR_F32_WS_COUNTERS 1024
 int vggt_linear_f32_ws(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, int M, int N, int K,
                        int act_in, int epi, float* out, int64_t ldo, const float* gamma, void* ws, size_t ws_bytes,
                        void* stream);

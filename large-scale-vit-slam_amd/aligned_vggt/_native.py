@@ -371,8 +371,9 @@ def linear_f32(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], o
     M, K = a.shape
     N_ = w.shape[0]
     assert a.dtype == torch.float32 and w.dtype == torch.float32 and w.shape[1] == K and out.shape == (M, N_)
-    # split-K scratch for skinny M (at most 16 splits of a 64-row-padded [M, N] fp32 slab)
-    need = 16 * ((M + 63) // 64) * 64 * N_
+    # split-K scratch for skinny M: the zeroed per-tile counter words, then at most 16
+    # splits of a 64-row-padded [M, N] fp32 slab
+    need = LINEAR_F32_WS_COUNTERS + 16 * ((M + 63) // 64) * 64 * N_
     ws = _split_ws(a.device, need) if M <= 256 else None
     rc = lib().vggt_linear_f32_ws(_p(a), _ld(a), _p(w), _ld(w), _p(bias), M, N_, K, act_in, epi, _p(out), _ld(out),
                                   _p(gamma), _p(ws), 0 if ws is None else ws.numel() * 4, _stream())
@@ -397,13 +398,18 @@ def _stream_key(device) -> tuple:
     return (device, torch.cuda.current_stream(device).stream_id)
 
 
+LINEAR_F32_WS_COUNTERS = 1024  # include/vggt_mi355x.h VGGT_LINEAR_F32_WS_COUNTERS
+
+
 def _split_ws(device, n_floats: int) -> torch.Tensor:
-    """Grow-only per-(device, stream) scratch for split-K partial sums."""
+    """Grow-only per-(device, stream) scratch for split-K partial sums; zero-filled
+    when (re)allocated (vggt_linear_f32_ws's tile counters at its start must start at
+    zero, and every call leaves them zero)."""
     key = _stream_key(device)
     table = scratch_table(_SPLIT_WS, "split_k")
     t = table.get(key)
     if t is None or t.numel() < n_floats:
-        t = torch.empty(n_floats, device=key[0], dtype=torch.float32)
+        t = torch.zeros(n_floats, device=key[0], dtype=torch.float32)
         table[key] = t
     return t
 

@@ -26,16 +26,23 @@ __global__ __launch_bounds__(256) void linear_f32_kernel(const float* __restrict
                                                          const float* __restrict__ W, int64_t ldw,
                                                          const float* __restrict__ bias, int M, int N, int K,
                                                          float* out, int64_t ldo, const float* __restrict__ gamma,
-                                                         int kchunk, float* __restrict__ part) {
+                                                         int kchunk, float* __restrict__ part, unsigned* cnt) {
   // split-K (part != NULL): block z covers K range [z*kchunk, (z+1)*kchunk) and
-  // stores its raw partial sums to part[z][M][N]; linear_f32_reduce applies
-  // bias and the epilogue.
+  // stores its raw partial sums to part[z][M][N].  With `cnt` (one zeroed word
+  // per 64 x 64 output tile) the LAST of the tile's split blocks to finish sums
+  // the partials in split order, applies bias and the epilogue and re-zeroes the
+  // word -- one launch, the same bits as linear_f32_reduce (the two-launch form
+  // used without `cnt`).
   const int kbeg = blockIdx.z * kchunk;
   const int kend = min(K, kbeg + kchunk);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int n0 = (blockIdx.x * 4 + wave) * 16;
-  if (n0 >= N) return;
+  // a wave past N computes clamped garbage it never stores (no early exit: with
+  // `cnt` every wave takes part in the tile's last-block protocol)
+  const bool active = n0 < N;
+  if (!active && !cnt) return;
+  const int Mfull = M;
   const int mbase = blockIdx.y * 64;
   A += (int64_t)mbase * lda;
   out += (int64_t)mbase * ldo;
@@ -117,20 +124,49 @@ __global__ __launch_bounds__(256) void linear_f32_kernel(const float* __restrict
   }
   // C[m = 16mt + 4q + i][n = n0 + r]
   const int n = n0 + r;
-  if (n >= N) return;
   if (part) {
-    float* pp = part + ((int64_t)blockIdx.z * gridDim.y * 64 + mbase) * N + n;
+    if (active && n < N) {
+      float* pp = part + ((int64_t)blockIdx.z * gridDim.y * 64 + mbase) * N + n;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      if (mt >= mt_n) break;
+      for (int mt = 0; mt < 4; ++mt) {
+        if (mt >= mt_n) break;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = mt * 16 + 4 * q + i;
-        if (m < M) pp[(int64_t)m * N] = acc[mt][i];
+        for (int i = 0; i < 4; ++i) {
+          const int m = mt * 16 + 4 * q + i;
+          if (m < M) pp[(int64_t)m * N] = acc[mt][i];
+        }
       }
     }
+    if (!cnt) return;
+    // this block's partials visible device-wide (every XCD's L2) before its ticket
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    __shared__ unsigned last;
+    unsigned* word = cnt + blockIdx.y * gridDim.x + blockIdx.x;
+    if (threadIdx.x == 0)
+      last = __hip_atomic_fetch_add(word, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.z - 1;
+    __syncthreads();
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const int64_t mstride = (int64_t)gridDim.y * 64 * N;
+    const int c0 = blockIdx.x * 64;
+    for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+      const int m = e >> 6, nn = c0 + (e & 63);
+      if (m >= M || nn >= N) continue;
+      const int64_t off = (int64_t)(mbase + m) * N + nn;
+      float v = 0.f;
+      for (int z = 0; z < (int)gridDim.z; ++z) v += part[z * mstride + off];
+      v += bias ? bias[nn] : 0.f;
+      float* op = out + (int64_t)m * ldo + nn;
+      if constexpr (EPI == VGGT_EPI_GELU_BF16) v = gelu_erf(v);
+      if constexpr (EPI == VGGT_EPI_RESID_F32) v = *op + gamma[nn] * v;
+      *op = v;
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(word, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    (void)Mfull;
     return;
   }
+  if (n >= N) return;
   const float bv = bias ? bias[n] : 0.f;
   const float g = (EPI == VGGT_EPI_RESID_F32) ? gamma[n] : 0.f;
 #pragma unroll
@@ -396,13 +432,17 @@ extern "C" int vggt_linear_f32_ws(const float* A, int64_t lda, const float* W, i
   int splits = 1;
   while (splits < 16 && blocks * splits * 2 <= 512 && K / (splits * 2) >= 128) splits *= 2;
   const int64_t mstride = (int64_t)gy * 64 * N;
-  if (splits > 1 && (!ws || ws_bytes < (size_t)splits * mstride * sizeof(float))) splits = 1;
+  // ws = [VGGT_LINEAR_F32_WS_COUNTERS zeroed tile words][partials]
+  const size_t cbytes = VGGT_LINEAR_F32_WS_COUNTERS * sizeof(unsigned);
+  if (splits > 1 && (!ws || ws_bytes < cbytes + (size_t)splits * mstride * sizeof(float))) splits = 1;
   const int kchunk = splits > 1 ? ((K + splits - 1) / splits + 15) / 16 * 16 : K;
-  float* part = splits > 1 ? (float*)ws : nullptr;
+  float* part = splits > 1 ? (float*)((char*)ws + cbytes) : nullptr;
+  // one launch (last block per tile combines) while the tile words fit
+  unsigned* cnt = (splits > 1 && blocks <= VGGT_LINEAR_F32_WS_COUNTERS) ? (unsigned*)ws : nullptr;
   const dim3 grid((N + 63) / 64, gy, splits);
   hipStream_t s = (hipStream_t)stream;
 #define LAUNCH(AI, E) \
-  linear_f32_kernel<AI, E><<<grid, 256, 0, s>>>(A, lda, W, ldw, bias, M, N, K, out, ldo, gamma, kchunk, part)
+  linear_f32_kernel<AI, E><<<grid, 256, 0, s>>>(A, lda, W, ldw, bias, M, N, K, out, ldo, gamma, kchunk, part, cnt)
   if (act_in == 0) {
     if (epi == VGGT_EPI_F32) LAUNCH(0, VGGT_EPI_F32);
     else if (epi == VGGT_EPI_GELU_BF16) LAUNCH(0, VGGT_EPI_GELU_BF16);
@@ -413,7 +453,7 @@ extern "C" int vggt_linear_f32_ws(const float* A, int64_t lda, const float* W, i
     else LAUNCH(1, VGGT_EPI_RESID_F32);
   }
 #undef LAUNCH
-  if (part) {
+  if (part && !cnt) {
     const int64_t total = (int64_t)M * N;
     const int rg = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
     if (epi == VGGT_EPI_F32) linear_f32_reduce<VGGT_EPI_F32><<<rg, 256, 0, s>>>(part, splits, mstride, M, N, bias, out, ldo, gamma);

@@ -41,6 +41,36 @@ def test_linear_f32(N, M, Nn, K, epi, act):
     assert _rel(out, ref) < 2e-6
 
 
+@pytest.mark.parametrize("M,Nn,K,epi", [(16, 512, 512, 3), (16, 2048, 512, 1), (1, 512, 2048, 2), (130, 1536, 1024, 3),
+                                         (16, 7, 256, 3), (256, 4096, 4096, 1)])
+def test_linear_f32_split_k_one_launch(N, M, Nn, K, epi):
+    """Skinny-M split-K (vggt_linear_f32_ws): the last split block of each output
+    tile combines the partials in split order in the same launch.  Bitwise
+    run-to-run (fixed order), within fp32 rounding of an fp64 reference, and the
+    scratch's tile counters are left zero for the next call."""
+    g = torch.Generator(device="cuda").manual_seed(M * Nn + K)
+    a = torch.randn(M, K, device="cuda", generator=g)
+    w = torch.randn(Nn, K, device="cuda", generator=g) / K ** 0.5
+    b = torch.randn(Nn, device="cuda", generator=g)
+    gam = torch.rand(Nn, device="cuda", generator=g) if epi == 2 else None
+    base = torch.randn(M, Nn, device="cuda", generator=g)
+    outs = []
+    for _ in range(3):
+        out = base.clone()
+        N.linear_f32(a, w, b, out, epi, gamma=gam)
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    ref = a.double() @ w.double().t() + b.double()
+    if epi == 1:
+        ref = F.gelu(ref)
+    if epi == 2:
+        ref = base.double() + gam.double() * ref
+    assert _rel(outs[0].double(), ref) < 2e-6, _rel(outs[0].double(), ref)
+    ws = N._split_ws(a.device, 0)
+    assert int(ws[:N.LINEAR_F32_WS_COUNTERS].view(torch.int32).count_nonzero()) == 0
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("G,H,nq,nk,D", [(1375, 8, 16, 5, 128), (2, 8, 1, 24, 64), (1, 16, 75, 75, 128),
                                           (3, 2, 7, 130 - 2, 32)])
