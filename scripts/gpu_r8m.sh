@@ -7,7 +7,7 @@ T=${1:-r8m}
 OUT=gpurun_out/$T
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 700 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_ring.py tests/test_gpu_fullsize.py -x -v -s \
+timeout -k 10 700 python -u -m pytest tests/test_gpu_small_kernels.py tests/test_gpu_pipeline.py tests/test_gpu_ring.py tests/test_gpu_fullsize.py -x -v -s \
   --timeout 600 --timeout-method thread > "$OUT/pytest.out" 2>&1 || exit $?
 tail -2 "$OUT/pytest.out"
 timeout -k 10 300 python -u bench.py --config 3 --steps 3 --warmup 2 --no-cpu-baseline > "$OUT/c3.out" 2> "$OUT/c3.err" || exit $?
