@@ -422,10 +422,21 @@ class ChunkPipeline:
         group_of = {i: gi for gi, g in enumerate(groups) for i in g}
         side = None
         if cuda:
-            side = self.__dict__.get("_align_stream")
+            streams = self.__dict__.setdefault("_align_streams", {})
+            side = streams.get(self.short_workgroups)
             if side is None:
                 lo, hi = torch.cuda.Stream.priority_range()
-                side = self._align_stream = torch.cuda.Stream(self.device, priority=hi)
+                if self.short_workgroups:
+                    # a dedicated high-priority stream, also short-workgroup: beside an encode its
+                    # GEMMs' tiles go to whichever CUs free up first instead of one persistent
+                    # workgroup per CU that starts only when its CU does
+                    from .. import _native as N
+                    from ..runtime import dedicated_stream
+                    side = dedicated_stream(self.device, priority=hi)
+                    N.set_stream_config(side.cuda_stream, 0, N.STREAM_SHORT_WORKGROUPS)
+                else:
+                    side = torch.cuda.Stream(self.device, priority=hi)
+                streams[self.short_workgroups] = side
         main = torch.cuda.current_stream(self.device) if cuda else None
         encs: Dict[int, dict] = {}
         ready: Dict[int, object] = {}

@@ -213,23 +213,23 @@ def _hip():
         _HIP.hipExtStreamCreateWithCUMask.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
                                                       ctypes.POINTER(ctypes.c_uint32)]
         _HIP.hipExtStreamCreateWithCUMask.restype = ctypes.c_int
-        _HIP.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
-        _HIP.hipStreamCreateWithFlags.restype = ctypes.c_int
+        _HIP.hipStreamCreateWithPriority.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint, ctypes.c_int]
+        _HIP.hipStreamCreateWithPriority.restype = ctypes.c_int
     return _HIP
 
 
-def dedicated_stream(device) -> "torch.cuda.ExternalStream":
+def dedicated_stream(device, priority: int = 0) -> "torch.cuda.ExternalStream":
     """A HIP stream of its own (non-blocking; not one of torch's pooled streams,
     which other users are handed too), as a torch ExternalStream -- for a
     per-stream library configuration (vggt_set_stream_config) that must apply to
-    this stream's work only."""
+    this stream's work only.  `priority` as torch.cuda.Stream's (lower = higher)."""
     import ctypes
     device = torch.device(device)
     s = ctypes.c_void_p()
     with torch.cuda.device(device):
-        rc = _hip().hipStreamCreateWithFlags(ctypes.byref(s), 1)  # hipStreamNonBlocking
+        rc = _hip().hipStreamCreateWithPriority(ctypes.byref(s), 1, int(priority))  # hipStreamNonBlocking
     if rc != 0:
-        raise RuntimeError(f"hipStreamCreateWithFlags failed ({rc})")
+        raise RuntimeError(f"hipStreamCreateWithPriority failed ({rc})")
     return torch.cuda.ExternalStream(s.value, device=device)
 
 
