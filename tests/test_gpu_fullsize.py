@@ -104,11 +104,13 @@ def test_vkitti_sequence_with_tail_reduced_depth(cuda, monkeypatch):
     print("154x518 sequence: hip vs bf16 oracle", e, "oracle fp32 vs bf16", e_ref)
     assert got["pose_enc"].shape == (1, N, 9) and got["depth"].shape[:2] == (1, N)
     assert got["chunk_sim3_alignment_enc"].shape == (1, 3, 8)
-    # north star on the Sim(3) chunk alignment; the rest through the random-init
-    # camera head / decoders, which amplify bf16 token rounding chaotically (the
-    # oracle's own bf16-vs-fp32 spread here: pose T ~6e-2, FoV ~3e-2): within 3e-2
-    # of the bf16 emulation or no further than twice that spread (as
-    # test_gpu_model.py's two-chunk test)
-    assert e["chunk_sim3"] < 1e-3, e
-    for k in ("frame_se3", "pose_T", "pose_fov", "depth"):
-        assert e[k] < 3e-2 or e[k] < 2.0 * e_ref[k], (k, e, e_ref)
+    # north star on the Sim(3) chunk alignment; per-output bars about 2x the values
+    # measured on MI355X (round 4: chunk_sim3 4.8e-4, frame_se3 8.0e-4, depth 1.4e-4,
+    # pose T 5.6e-2, FoV 4.4e-2).  The poses pass through the random-init camera head,
+    # which amplifies bf16 token rounding (the oracle's own bf16-vs-fp32 spread here:
+    # T 5.6e-2, FoV 3.2e-2), so they are ALSO held within twice that spread.
+    bars = {"chunk_sim3": 1e-3, "frame_se3": 2e-3, "depth": 5e-4, "pose_T": 1e-1, "pose_fov": 8e-2}
+    for k, bar in bars.items():
+        assert e[k] < bar, (k, e, bar)
+    for k in ("pose_T", "pose_fov"):
+        assert e[k] < 2.0 * e_ref[k], (k, e, e_ref)
