@@ -350,8 +350,9 @@ def test_pipeline_grouped_encode_matches(models, H, W, N, w, ov):
             assert e < 1e-5, (g, k, e)
 
 
-@pytest.mark.parametrize("conv,reorder,tol", [("bf16x3pre", True, 1e-4), ("bf16x3pre", False, 1e-4),
-                                              ("bf16x3", True, 1e-4), ("fp32", True, 2e-6)])
+# measured (round 4): 2.6e-6 for the split-bf16 convolutions, 4.6e-7 on exact fp32
+@pytest.mark.parametrize("conv,reorder,tol", [("bf16x3pre", True, 1e-5), ("bf16x3pre", False, 1e-5),
+                                              ("bf16x3", True, 1e-5), ("fp32", True, 2e-6)])
 def test_dpt_matches_transformers_depth_anything(golden, monkeypatch, conv, reorder, tol):
     """HIP DPTHead (pos_embed off) vs the in-container transformers
     Depth-Anything neck + head run with the same weights (tests/golden/dpt_hf.npz,

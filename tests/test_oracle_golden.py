@@ -90,8 +90,9 @@ def test_dpt_stages_match_transformers_depth_anything(golden):
     with torch.no_grad():
         O.dpt_head(sd, "", [toks] * 4, imgs, 5, "exp", pos_embed=False, stages=st)
     for k in [f"reassemble{i}" for i in range(4)] + [f"rn{i}" for i in range(4)] + [f"fused{j}" for j in range(4)]:
-        np.testing.assert_allclose(st[k].numpy(), g[k], rtol=1e-4, atol=2e-5, err_msg=k)
-    np.testing.assert_allclose(st["head_pre"][:, :1].numpy(), g["head_pre"], rtol=1e-4, atol=2e-5)
+        # measured 2e-7 .. 6e-7 rel-L2 per stage (max abs 6.6e-7): fp32 summation order only
+        np.testing.assert_allclose(st[k].numpy(), g[k], rtol=1e-5, atol=2e-6, err_msg=k)
+    np.testing.assert_allclose(st["head_pre"][:, :1].numpy(), g["head_pre"], rtol=1e-5, atol=2e-6)
     np.testing.assert_allclose(torch.sigmoid(st["head_pre"][:, 0]).numpy(), g["out_sigmoid"], rtol=1e-5, atol=1e-6)
 
 
