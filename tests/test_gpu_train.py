@@ -512,6 +512,9 @@ def test_alignment_head_gradients_vs_reference_fixture(N, golden):
     print("HIP vs reference bf16-mixed gradients, worst:", [(k, round(e_bf[k], 5), round(e_32[k], 5)) for k in worst])
     print("median rel error vs bf16 ref %.3e, vs fp32 ref %.3e" % (float(np.median(list(e_bf.values()))),
                                                                   float(np.median(list(e_32.values())))))
+    # measured on MI355X (round 4): worst parameter 1.4e-2 vs the bf16-mixed reference and 1.5e-2 vs the fp32 one
+    # (k_norm biases: tiny gradients), median 2.2e-3 / 2.1e-3, loss ratio 3.3e-4
     assert abs(float(loss) / float(g["bf16_loss"]) - 1) < 1e-3
-    bad = {k: (e_bf[k], e_32[k]) for k in e_bf if not (e_bf[k] < 5e-2 or e_32[k] < 5e-2)}
+    bad = {k: (e_bf[k], e_32[k]) for k in e_bf if not (e_bf[k] < 3e-2 and e_32[k] < 3e-2)}
     assert not bad, bad
+    assert float(np.median(list(e_bf.values()))) < 5e-3 and float(np.median(list(e_32.values()))) < 5e-3
