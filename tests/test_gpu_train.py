@@ -325,7 +325,9 @@ def _grad_compare(head, sd_bf, sd_32, report):
             continue
         e, e32, eref = _rel(p.grad, gr), _rel(p.grad, g32), _rel(gr, g32)
         errs[name] = (e, e32, eref)
-    bad = {k: v for k, v in errs.items() if not (v[0] < 5e-2 or v[1] < 2.0 * v[2])}
+    # measured on MI355X (round 4): worst 3.2e-2 vs the bf16 emulation (alpha, whose fp32 distance is 6.4e-3)
+    # and 3.3e-2 vs fp32 (k_norm biases, where the emulation's own bf16-vs-fp32 spread is 2.7e-2 .. 3.2e-2)
+    bad = {k: v for k, v in errs.items() if not (v[0] < 4e-2 and v[1] < max(4e-2, 1.5 * v[2]))}
     worst = sorted(errs.items(), key=lambda kv: -kv[1][0])[:8]
     print(report, "worst (hip-vs-bf16emu, hip-vs-fp32, ref-bf16-vs-fp32):", worst)
     assert not bad, bad
