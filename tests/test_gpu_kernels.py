@@ -281,7 +281,10 @@ def _attention_vs_torch(N, D, H, batch, n):
     N.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, batch, H, n, n, D, n, n, n)
     t = qkv.float().view(batch, n, 3, H, D).permute(2, 0, 3, 1, 4)
     ref = _ref_attn(t[0], t[1], t[2], D ** -0.5).permute(0, 2, 1, 3).reshape(batch * n, C)
-    assert _rel(o, ref) < 1e-2, _rel(o, ref)
+    e = _rel(o, ref)
+    print(f"attention D={D} H={H} batch={batch} n={n}: rel-L2 vs fp32 {e:.2e}")
+    # bf16 P and bf16 output: ~2-3e-3 (round 4); the bar is about 2x that
+    assert e < 6e-3, e
 
 
 @pytest.mark.parametrize("waves,n,D", [(8, 4100, 64), (8, 5000, 64), (8, 8191, 64), (8, 4100, 128), (2, 65, 64), (2, 1374, 64),
@@ -299,7 +302,9 @@ def test_attention_eight_wave_form(N, waves, n, D):
         N.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, 1, H, n, n, D, n, n, n)
         t = qkv.float().view(1, n, 3, H, D).permute(2, 0, 3, 1, 4)
         ref = _ref_attn(t[0], t[1], t[2], D ** -0.5).permute(0, 2, 1, 3).reshape(n, C)
-        assert _rel(o, ref) < 1e-2, _rel(o, ref)
+        e = _rel(o, ref)
+        print(f"attention {waves}-wave D={D} n={n}: rel-L2 vs fp32 {e:.2e}")
+        assert e < 6e-3, e
     finally:
         N.tune(N.TUNE_ATTN_WAVES, prev)
 
