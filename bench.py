@@ -413,7 +413,7 @@ def bench_full(args, world, rank, dev):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
     recurrence = None
-    if args.workload == "sequence":
+    if args.workload == "sequence" and os.environ.get("VGGT_RECURRENCE_PROBE", "1") != "0":
         recurrence = _recurrence_probe(pipe, step, n_chunks_step, dt / args.steps * 1e3, world)
     if world > 1:
         dist.destroy_process_group()
