@@ -24,7 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _native as N
-from ..runtime import Workspace, pack_linear, round_up
+from ..runtime import Workspace, pack_linear, round_up, yield_point
 from .layers import Block, RopeTables
 
 _RESNET_MEAN = (0.485, 0.456, 0.406)
@@ -185,6 +185,8 @@ class Aggregator(nn.Module):
                         x)
         ready = False
         for j, blk in enumerate(dino.blocks):
+            if j % 4 == 0:
+                yield_point()  # the multi-GPU pipeline's encode pauses here while an alignment runs
             nxt = dino.blocks[j + 1].norm1 if j + 1 < len(dino.blocks) else None
             ready = blk.forward_rows(x, M, (F_, P, P), None, ws, tag="dino_attn", xn_ready=ready, next_norm=nxt)
 
@@ -198,6 +200,7 @@ class Aggregator(nn.Module):
         # each block's last residual add also writes the next block's norm1(y)
         ready = False
         for i in range(self.depth):
+            yield_point()
             o = outs[i].view(M, 2 * C) if i in outs else None
             ready = self.frame_blocks[i].forward_rows(y, M, (F_, P, P), rope, ws,
                                                       out2=o[:, :C] if o is not None else None, tag="frame_attn",

@@ -159,7 +159,8 @@ class ChunkPipeline:
 
     def __init__(self, model, group=None, device=None, gather_dense: bool = False,
                  encode_group: Optional[int] = None, overlap_align: Optional[bool] = None,
-                 time_align: bool = False, short_workgroups: Optional[bool] = None):
+                 time_align: bool = False, short_workgroups: Optional[bool] = None,
+                 gate_encode: Optional[bool] = None):
         self.model = model
         # one rank: align chunk i on the side stream while the next encode group
         # runs (the ring's schedule with the baton kept on the device);
@@ -183,6 +184,14 @@ class ChunkPipeline:
         if short_workgroups is None:
             short_workgroups = os.environ.get("VGGT_RING_SHORT_WG", "1") != "0"
         self.short_workgroups = short_workgroups
+        # gate_encode: in the ring's schedule the encode stream pauses at its yield points
+        # (between transformer blocks, before each head) while an alignment runs
+        # (runtime.EncodeGate: one signal word, hipStreamWriteValue32 / hipStreamWaitValue32),
+        # so the alignment -- the recurrence's critical path -- runs alone after at most one
+        # yield interval of sharing.  VGGT_RING_GATE=0 turns it off.
+        if gate_encode is None:
+            gate_encode = os.environ.get("VGGT_RING_GATE", "1") != "0"
+        self.gate_encode = gate_encode
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -299,7 +308,7 @@ class ChunkPipeline:
         self.align_events = []
         if self.world == 1 and not self.overlap_align:
             mine = self._run_local(images, chunks, num_overlap, keys, memory_shape, B)
-        elif ((self.reserve_cus > 0 or self.short_workgroups) and self.device is not None
+        elif ((self.reserve_cus > 0 or self.short_workgroups or self.gate_encode) and self.device is not None
               and torch.device(self.device).type == "cuda"):
             enc_stream = self._encode_stream()
             cur = torch.cuda.current_stream(self.device)
@@ -438,9 +447,14 @@ class ChunkPipeline:
                     side = torch.cuda.Stream(self.device, priority=hi)
                 streams[self.short_workgroups] = side
         main = torch.cuda.current_stream(self.device) if cuda else None
+        gate = None
+        if cuda and self.gate_encode and main.cuda_stream != 0:
+            from ..runtime import EncodeGate
+            gate = self.__dict__.get("_gate")
+            if gate is None:
+                gate = self._gate = EncodeGate(self.device)
         encs: Dict[int, dict] = {}
         ready: Dict[int, object] = {}
-        enqueued = 0
 
         def enqueue(gi):
             g = groups[gi]
@@ -455,7 +469,27 @@ class ChunkPipeline:
 
         mine: Dict[int, dict] = {}
         sends = []
+        gate_ctx = contextlib.nullcontext()
+        if gate is not None:
+            from ..runtime import gated
+            gate_ctx = gated(main, gate)
+        with gate_ctx:
+            self._ring_loop(own, group_of, groups, enqueue, encs, ready, side, cuda, chunks, num_overlap, keys,
+                            B, P1, C, memory_shape, mine, sends, gate)
+        for works, _ in sends:
+            for w in works:
+                w.wait()
+        if cuda:
+            main.wait_stream(side)
+            for v in mine.values():
+                _record_stream(v, main)
+        return mine
+
+    def _ring_loop(self, own, group_of, groups, enqueue, encs, ready, side, cuda, chunks, num_overlap, keys,
+                   B, P1, C, memory_shape, mine, sends, gate) -> None:
+        W, n = self.world, len(chunks)
         local = None
+        enqueued = 0
         for i in own:
             gi = group_of[i]
             while enqueued <= min(gi + 1, len(groups) - 1):  # this group and the next one queued
@@ -480,24 +514,20 @@ class ChunkPipeline:
                     else:
                         ctx_in = local
                     ctx = self._ctx_from(ctx_in, B, memory_shape)
+                if gate is not None:
+                    gate.begin(side)  # the encode stream pauses at its next yield point
                 ev0 = self._tick()
                 pred = self.model.align_chunk(enc, num_overlap, ctx)
                 if ev0 is not None:
                     self.align_events.append((i, ev0, self._tick()))
+                if gate is not None:
+                    gate.end(side)
                 if i + 1 < n:
                     if W > 1:
                         sends.append(self._isend(pred, (i + 1) % W, keys))
                     else:
                         local = {k: (pred[k][-1] if isinstance(pred[k], list) else pred[k]) for k in keys}
                 mine[i] = self._summary(pred, len(chunks[i]))
-        for works, _ in sends:
-            for w in works:
-                w.wait()
-        if cuda:
-            main.wait_stream(side)
-            for v in mine.values():
-                _record_stream(v, main)
-        return mine
 
     def _tick(self):
         """A timing event on the current stream (``time_align`` on a HIP device), else None."""

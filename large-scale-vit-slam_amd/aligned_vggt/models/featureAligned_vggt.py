@@ -23,7 +23,7 @@ from ..backbone.camera_head import CameraHead
 from ..backbone.dpt_head import DPTHead
 from ..backbone.track_head import TrackHead
 from ..heads.alignment_head import AlignmentHead
-from ..runtime import private_scratch, round_up
+from ..runtime import private_scratch, round_up, yield_point
 from ..utils.data import extri_to_pose_encoding, pose_encoding_to_extri
 from ..utils.geometry import averagePoseEncodings, closed_form_inverse_se3
 from ..utils.pose_enc import extri_intri_to_pose_encoding, pose_encoding_to_extri_intri
@@ -116,13 +116,18 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
         B, S, C, H, W = images.shape
         toks, patch_start_idx = self.aggregator(images, keep_layers=self.intermediate_layer_indices)
         enc = {"images": images, "tokens": toks, "patch_start_idx": patch_start_idx}
+        # yield points: the multi-GPU pipeline's encode pauses there while an alignment runs (runtime.EncodeGate)
         if self.camera_head is not None:
+            yield_point()
             enc["cam_pose_enc"] = self.camera_head(toks)[-1]
         if self.depth_head is not None:
+            yield_point()
             enc["depth"], enc["depth_conf"] = self.depth_head(toks, images=images, patch_start_idx=patch_start_idx)
         if self.point_head is not None:
+            yield_point()
             enc["points"], enc["points_conf"] = self.point_head(toks, images=images, patch_start_idx=patch_start_idx)
         if _ALIGN_PREFIX and not self.alignment_head.training and images.is_cuda:
+            yield_point()
             # the alignment head's context-free prefix, as (B, S*(P+1), C) rows so a
             # grouped encode's result splits per chunk along dim 0
             P1 = toks[-1].shape[2] + 1

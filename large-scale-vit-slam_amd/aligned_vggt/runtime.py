@@ -215,7 +215,96 @@ def _hip():
         _HIP.hipExtStreamCreateWithCUMask.restype = ctypes.c_int
         _HIP.hipStreamCreateWithPriority.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint, ctypes.c_int]
         _HIP.hipStreamCreateWithPriority.restype = ctypes.c_int
+        _HIP.hipExtMallocWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+        _HIP.hipExtMallocWithFlags.restype = ctypes.c_int
+        _HIP.hipFree.argtypes = [ctypes.c_void_p]
+        _HIP.hipFree.restype = ctypes.c_int
+        _HIP.hipStreamWaitValue32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint,
+                                              ctypes.c_uint32]
+        _HIP.hipStreamWaitValue32.restype = ctypes.c_int
+        _HIP.hipStreamWriteValue32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint]
+        _HIP.hipStreamWriteValue32.restype = ctypes.c_int
     return _HIP
+
+
+class EncodeGate:
+    """A device-side pause for the multi-GPU pipeline's encode stream while an
+    alignment runs: one 32-bit signal word (hipExtMallocWithFlags,
+    hipMallocSignalMemory).  The alignment stream writes 1 when it starts a
+    chunk (after its device-side waits for the baton and the chunk's encode)
+    and 0 when it is done (hipStreamWriteValue32); the encode stream, at its
+    yield points (`yield_point`, between transformer blocks and heads), waits
+    for 0 (hipStreamWaitValue32).  An alignment therefore shares the GPU with
+    at most one yield interval of encode work and then runs alone.  No cycle:
+    the word goes to 1 only after the chunk's own encode has finished, and the
+    alignment never waits on the encode stream after that."""
+
+    def __init__(self, device):
+        import ctypes
+        self.device = torch.device(device)
+        p = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            rc = _hip().hipExtMallocWithFlags(ctypes.byref(p), 64, 0x2)  # hipMallocSignalMemory
+            if rc != 0:
+                raise RuntimeError(f"hipExtMallocWithFlags(hipMallocSignalMemory) failed ({rc})")
+            self.ptr = p.value
+            s = torch.cuda.current_stream(self.device)
+            self._write(s.cuda_stream, 0)
+            s.synchronize()
+
+    def _write(self, stream: int, v: int) -> None:
+        import ctypes
+        rc = _hip().hipStreamWriteValue32(ctypes.c_void_p(stream), ctypes.c_void_p(self.ptr), v, 0)
+        if rc != 0:
+            raise RuntimeError(f"hipStreamWriteValue32 failed ({rc})")
+
+    def begin(self, stream) -> None:
+        """On the alignment stream, after its waits: the encode pauses at its next yield point."""
+        self._write(stream.cuda_stream, 1)
+
+    def end(self, stream) -> None:
+        self._write(stream.cuda_stream, 0)
+
+    def wait(self, stream: int) -> None:
+        import ctypes
+        rc = _hip().hipStreamWaitValue32(ctypes.c_void_p(stream), ctypes.c_void_p(self.ptr), 0, 0x1,
+                                         0xFFFFFFFF)  # hipStreamWaitValueEq
+        if rc != 0:
+            raise RuntimeError(f"hipStreamWaitValue32 failed ({rc})")
+
+    def close(self) -> None:
+        if getattr(self, "ptr", None):
+            import ctypes
+            torch.cuda.synchronize(self.device)
+            _hip().hipFree(ctypes.c_void_p(self.ptr))
+            self.ptr = None
+
+
+_GATE = threading.local()
+
+
+@contextlib.contextmanager
+def gated(stream, gate: "EncodeGate"):
+    """Within the block, `yield_point()` calls made while `stream` is current
+    enqueue a wait on `gate` (the encode stream of the pipeline's ring)."""
+    prev = getattr(_GATE, "cur", None)
+    _GATE.cur = (stream.cuda_stream, gate)
+    try:
+        yield
+    finally:
+        _GATE.cur = prev
+
+
+def yield_point() -> None:
+    """A place in the encode (between transformer blocks, before each head)
+    where a gated encode stream pauses while an alignment runs; a no-op
+    otherwise."""
+    cur = getattr(_GATE, "cur", None)
+    if cur is None:
+        return
+    handle, gate = cur
+    if torch.cuda.current_stream(gate.device).cuda_stream == handle:
+        gate.wait(handle)
 
 
 def dedicated_stream(device, priority: int = 0) -> "torch.cuda.ExternalStream":
