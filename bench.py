@@ -445,33 +445,36 @@ def _recurrence_probe(pipe, step, n_chunks, t1_ms, world):
     (align on the side stream while the next encode group runs: t_align under
     load, the regime of every W > 1 rank).  At W = 1 (b) is the W = 1 ring
     schedule (overlap_align), whose sequence time is reported beside: with the
-    ring's default short-workgroup encode stream, with the persistent GEMMs
-    (ChunkPipeline.short_workgroups off) and, for VGGT_PROBE_RESERVE=r,..., with
-    the encodes masked off r CUs (ChunkPipeline.reserve_cus).  bound_frac_* =
+    ring's defaults (short-workgroup streams, the encode gated while an
+    alignment runs), without the gate, with the persistent GEMMs and no gate,
+    and, for VGGT_PROBE_RESERVE=r,..., with the encodes masked off r CUs.  bound_frac_* =
     n_chunks x t_align over the overlapped sequence time / 8: the 8-rank ring's
     critical path against its encode share (<= 1: the encodes bound it)."""
     import statistics
     pipe.time_align = True
     out = {"n_chunks": n_chunks}
-    # (name, overlap_align, reserve_cus, short_workgroups); None = the pipeline's setting
+    # (name, overlap_align, reserve_cus, short_workgroups, gate_encode); None = the pipeline's setting
     rsvs = [int(x) for x in os.environ.get("VGGT_PROBE_RESERVE", "").split(",") if x]
-    modes = ((("alone", False, 0, None), ("under_load", True, 0, True), ("under_load_persistent", True, 0, False))
-             + tuple(("under_load_reserved%d" % r, True, r, True) for r in rsvs)
-             if world == 1 else (("under_load", None, None, None),))
-    for name, ov_mode, rsv, short in modes:
-        keep, keep_rsv, keep_short = pipe.overlap_align, pipe.reserve_cus, pipe.short_workgroups
+    modes = ((("alone", False, 0, None, None), ("under_load", True, 0, True, True),
+              ("under_load_ungated", True, 0, True, False), ("under_load_persistent", True, 0, False, False))
+             + tuple(("under_load_reserved%d" % r, True, r, True, False) for r in rsvs)
+             if world == 1 else (("under_load", None, None, None, None),))
+    for name, ov_mode, rsv, short, gate in modes:
+        keep = (pipe.overlap_align, pipe.reserve_cus, pipe.short_workgroups, pipe.gate_encode)
         if ov_mode is not None:
             pipe.overlap_align = ov_mode
         if rsv is not None:
             pipe.reserve_cus = rsv
         if short is not None:
             pipe.short_workgroups = short
+        if gate is not None:
+            pipe.gate_encode = gate
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         step()
         torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) * 1e3
-        pipe.overlap_align, pipe.reserve_cus, pipe.short_workgroups = keep, keep_rsv, keep_short
+        pipe.overlap_align, pipe.reserve_cus, pipe.short_workgroups, pipe.gate_encode = keep
         ms = pipe.align_ms()
         out["t_align_ms_%s_median" % name] = round(statistics.median(ms), 3) if ms else None
         out["t_align_ms_%s_max" % name] = round(max(ms), 3) if ms else None
@@ -484,9 +487,9 @@ def _recurrence_probe(pipe, step, n_chunks, t1_ms, world):
         out["bound_frac_of_T1_over_8"] = round(n_chunks * t_load / (t1_ms / 8), 3)
         # the same bound against the encode time of that configuration (the W = 1
         # overlapped sequence on its encode stream, / 8)
-        for name, _, r, _ in modes:
+        for name, ov_mode, r, _, _ in modes:
             t = out.get("t_align_ms_%s_median" % name)
-            if (r or name == "under_load") and t:
+            if ov_mode and t:
                 out["bound_frac_%s" % name] = round(n_chunks * t / (out["sequence_ms_%s" % name] / 8), 3)
     return out
 
