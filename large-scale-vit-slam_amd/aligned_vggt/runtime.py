@@ -244,7 +244,7 @@ class EncodeGate:
         self.device = torch.device(device)
         p = ctypes.c_void_p()
         with torch.cuda.device(self.device):
-            rc = _hip().hipExtMallocWithFlags(ctypes.byref(p), 64, 0x2)  # hipMallocSignalMemory
+            rc = _hip().hipExtMallocWithFlags(ctypes.byref(p), 8, 0x2)  # hipMallocSignalMemory: one 8-byte signal
             if rc != 0:
                 raise RuntimeError(f"hipExtMallocWithFlags(hipMallocSignalMemory) failed ({rc})")
             self.ptr = p.value
