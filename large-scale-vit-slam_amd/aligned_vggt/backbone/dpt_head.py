@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 
 from .. import _native as N
-from ..runtime import Workspace
+from ..runtime import Workspace, yield_point
 
 
 def _make_sincos(embed_dim: int, pos: torch.Tensor, omega_0: float = 100) -> torch.Tensor:
@@ -360,7 +360,10 @@ class DPTHead(nn.Module):
         hw = ph * pw
         ws = Workspace.get(dev)
         feats = []
+        # yield points (the multi-GPU pipeline's gated encode pauses there while an
+        # alignment runs): every reassemble layer, fusion block and the output stage
         for li, layer_idx in enumerate(self.intermediate_layer_idx):
+            yield_point()
             tk = aggregated_tokens_list[layer_idx]
             P, Cin = tk.shape[2], tk.shape[3]
             xl = ws.buf("dpt_ln", F_ * hw, Cin)
@@ -381,10 +384,15 @@ class DPTHead(nn.Module):
         l2 = _conv(feats[1], sc.layer2_rn, split="relu")
         l3 = _conv(feats[2], sc.layer3_rn, split="relu")
         l4 = _conv(feats[3], sc.layer4_rn, split="relu")
+        yield_point()
         out = self._fuse(sc.refinenet4, l4, None, (l3.h, l3.w))
+        yield_point()
         out = self._fuse(sc.refinenet3, out, l3, (l2.h, l2.w))
+        yield_point()
         out = self._fuse(sc.refinenet2, out, l2, (l1.h, l1.w))
+        yield_point()
         out = self._fuse(sc.refinenet1, out, l1, None, f32=False, split="plain")
+        yield_point()
         out = _conv(out, sc.output_conv1)
         Ho, Wo = int(ph * self.patch_size / self.down_ratio), int(pw * self.patch_size / self.down_ratio)
         c2 = sc.output_conv2[0]
