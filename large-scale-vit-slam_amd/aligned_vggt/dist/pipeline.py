@@ -431,11 +431,14 @@ class ChunkPipeline:
         group_of = {i: gi for gi, g in enumerate(groups) for i in g}
         side = None
         if cuda:
+            # the alignment's own GEMMs: persistent when the encode is gated (the
+            # alignment then has the GPU to itself after one yield interval), else short
+            align_short = self.short_workgroups and not self.gate_encode
             streams = self.__dict__.setdefault("_align_streams", {})
-            side = streams.get(self.short_workgroups)
+            side = streams.get(align_short)
             if side is None:
                 lo, hi = torch.cuda.Stream.priority_range()
-                if self.short_workgroups:
+                if align_short:
                     # a dedicated high-priority stream, also short-workgroup: beside an encode its
                     # GEMMs' tiles go to whichever CUs free up first instead of one persistent
                     # workgroup per CU that starts only when its CU does
@@ -445,7 +448,7 @@ class ChunkPipeline:
                     N.set_stream_config(side.cuda_stream, 0, N.STREAM_SHORT_WORKGROUPS)
                 else:
                     side = torch.cuda.Stream(self.device, priority=hi)
-                streams[self.short_workgroups] = side
+                streams[align_short] = side
         main = torch.cuda.current_stream(self.device) if cuda else None
         gate = None
         if cuda and self.gate_encode and main.cuda_stream != 0:
