@@ -185,8 +185,7 @@ class Aggregator(nn.Module):
                         x)
         ready = False
         for j, blk in enumerate(dino.blocks):
-            if j % 4 == 0:
-                yield_point()  # the multi-GPU pipeline's encode pauses here while an alignment runs
+            yield_point()  # the multi-GPU pipeline's gated encode pauses here while an alignment runs
             nxt = dino.blocks[j + 1].norm1 if j + 1 < len(dino.blocks) else None
             ready = blk.forward_rows(x, M, (F_, P, P), None, ws, tag="dino_attn", xn_ready=ready, next_norm=nxt)
 
@@ -206,6 +205,7 @@ class Aggregator(nn.Module):
                                                       out2=o[:, :C] if o is not None else None, tag="frame_attn",
                                                       xn_ready=ready, next_norm=self.global_blocks[i].norm1)
             nxt = self.frame_blocks[i + 1].norm1 if i + 1 < self.depth else None
+            yield_point()
             ready = self.global_blocks[i].forward_rows(y, M, (B, S * P, S * P), rope, ws,
                                                        out2=o[:, C:] if o is not None else None, tag="global_attn",
                                                        xn_ready=ready, next_norm=nxt)
