@@ -456,7 +456,8 @@ def _recurrence_probe(pipe, step, n_chunks, t1_ms, world):
     # (name, overlap_align, reserve_cus, short_workgroups, gate_encode); None = the pipeline's setting
     rsvs = [int(x) for x in os.environ.get("VGGT_PROBE_RESERVE", "").split(",") if x]
     modes = ((("alone", False, 0, None, None), ("under_load", True, 0, True, True),
-              ("under_load_ungated", True, 0, True, False), ("under_load_persistent", True, 0, False, False))
+              ("under_load_ungated", True, 0, True, False), ("under_load_persistent", True, 0, False, False),
+              ("under_load_gated_persistent", True, 0, False, True))
              + tuple(("under_load_reserved%d" % r, True, r, True, False) for r in rsvs)
              if world == 1 else (("under_load", None, None, None, None),))
     for name, ov_mode, rsv, short, gate in modes:
