@@ -445,9 +445,10 @@ def _recurrence_probe(pipe, step, n_chunks, t1_ms, world):
     (align on the side stream while the next encode group runs: t_align under
     load, the regime of every W > 1 rank).  At W = 1 (b) is the W = 1 ring
     schedule (overlap_align), whose sequence time is reported beside: with the
-    ring's defaults (short-workgroup streams, the encode gated while an
-    alignment runs), without the gate, with the persistent GEMMs and no gate,
-    and, for VGGT_PROBE_RESERVE=r,..., with the encodes masked off r CUs.  bound_frac_* =
+    ring's defaults (the encode gated while an alignment runs, persistent
+    GEMMs), gated with short-workgroup streams, ungated short-workgroup, ungated
+    persistent (the round-3 schedule) and, for VGGT_PROBE_RESERVE=r,..., with
+    the encodes masked off r CUs.  bound_frac_* =
     n_chunks x t_align over the overlapped sequence time / 8: the 8-rank ring's
     critical path against its encode share (<= 1: the encodes bound it)."""
     import statistics
@@ -455,9 +456,9 @@ def _recurrence_probe(pipe, step, n_chunks, t1_ms, world):
     out = {"n_chunks": n_chunks}
     # (name, overlap_align, reserve_cus, short_workgroups, gate_encode); None = the pipeline's setting
     rsvs = [int(x) for x in os.environ.get("VGGT_PROBE_RESERVE", "").split(",") if x]
-    modes = ((("alone", False, 0, None, None), ("under_load", True, 0, True, True),
-              ("under_load_ungated", True, 0, True, False), ("under_load_persistent", True, 0, False, False),
-              ("under_load_gated_persistent", True, 0, False, True))
+    modes = ((("alone", False, 0, None, None), ("under_load", True, 0, None, None),
+              ("under_load_gated_short", True, 0, True, True), ("under_load_ungated_short", True, 0, True, False),
+              ("under_load_ungated", True, 0, False, False))
              + tuple(("under_load_reserved%d" % r, True, r, True, False) for r in rsvs)
              if world == 1 else (("under_load", None, None, None, None),))
     for name, ov_mode, rsv, short, gate in modes:

@@ -174,15 +174,14 @@ class ChunkPipeline:
         # over the XCDs), so the alignment recurrence's kernels never queue behind a
         # full-chip encode launch; VGGT_ALIGN_RESERVE_CUS sets the default (0: off)
         self.reserve_cus = int(os.environ.get("VGGT_ALIGN_RESERVE_CUS", "0"))
-        # short_workgroups: in the ring's schedule the encodes run on a dedicated
-        # stream configured for short workgroups (vggt_set_stream_config: no
+        # short_workgroups: the ring's encodes (and, ungated, its alignments) run on
+        # dedicated streams configured for short workgroups (vggt_set_stream_config: no
         # persistent GEMM forms, whose one-workgroup-per-CU grids hold every CU for a
-        # whole launch), so the alignment's kernels on the high-priority stream find
-        # CUs within microseconds: t_align beside an encode 7.6 -> 5.1 ms per 154x518
-        # chunk for +10 % encode time, the 8-rank bound 43 t_align / (T1/8) 2.1 -> 1.3
-        # (DESIGN.md §8c).  VGGT_RING_SHORT_WG=0 turns it off.
+        # whole launch).  Ungated that took t_align beside an encode 7.6 -> 5.4 ms per
+        # 154x518 chunk; with the gate below it no longer helps (3.6 vs 3.7 ms) and costs
+        # the encode 7 %, so it is off by default.  VGGT_RING_SHORT_WG=1.
         if short_workgroups is None:
-            short_workgroups = os.environ.get("VGGT_RING_SHORT_WG", "1") != "0"
+            short_workgroups = os.environ.get("VGGT_RING_SHORT_WG", "0") == "1"
         self.short_workgroups = short_workgroups
         # gate_encode: in the ring's schedule the encode stream pauses at its yield points
         # (between transformer blocks, before each head) while an alignment runs
