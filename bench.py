@@ -131,6 +131,24 @@ def cpu_baseline(threads: int):
     return out
 
 
+def _measured_row(row: str, threads: int):
+    """A BASELINE.md §3 CPU row measured on whole chunks by scripts/cpu_baseline_full.py
+    (1 warm-up + >= 3 timed runs, median; profiles/cpu_baseline_full.json), or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "cpu_baseline_full.json")) as fh:
+            full = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    r = full.get("rows", {}).get(f"{row}_t{threads}")
+    if not r or r.get("runs", 0) < 3:
+        return None
+    return {"value": r["chunks_per_s"], "unit": "chunks/s", "cores": threads, "kind": "port",
+            "host_cpu": full.get("host_cpu"), "host_logical_cpus": full.get("host_logical_cpus"),
+            "sample": f"oracle fp32 CPU (reference numerics), {r['workload']}: {r['runs']} timed whole chunks "
+                      f"{r['runs_s']} s after a warm-up, median {r['median_s_per_chunk']} s/chunk "
+                      f"(profiles/cpu_baseline_full.json)"}
+
+
 def _cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -565,7 +583,8 @@ def bench_point(args, world, rank, dev):
                      "flops_per_launch": fl["global_attn_launch"], "traffic": None},
     }
     if cpu_sd is not None:
-        line["cpu_baseline"] = cpu_baseline_point(cpu_sd, S, H, W, args.cpu_threads, args.cpu_runs)
+        measured = _measured_row("C1", args.cpu_threads) if (S, H, W) == (8, 518, 518) else None
+        line["cpu_baseline"] = measured or cpu_baseline_point(cpu_sd, S, H, W, args.cpu_threads, args.cpu_runs)
     print(json.dumps(line), flush=True)
 
 
