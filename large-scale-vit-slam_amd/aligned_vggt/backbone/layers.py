@@ -20,7 +20,7 @@ import torch
 import torch.nn as nn
 
 from .. import _native as N
-from ..runtime import Workspace, pack_linear
+from ..runtime import Workspace, pack_linear, yield_point
 
 
 class LayerScale(nn.Module):
@@ -178,6 +178,7 @@ class Block(nn.Module):
                           rp.cos if rp else None, rp.sin if rp else None)
         ao = ws.buf("blk_ao", M, C, torch.bfloat16)
         nb, rows, n = groups
+        yield_point()  # a gated encode (multi-GPU ring) pauses here while an alignment runs
         N.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], ao, nb, H, n, n, D, rows, rows, rows, tag=tag)
         w, b = pack_linear(self.attn.proj)
         fal = _FUSED_ADD_LN if M >= _FUSED_ADD_LN_MIN_ROWS else 0
@@ -192,6 +193,7 @@ class Block(nn.Module):
             N.layernorm(xs, self.norm2.weight, self.norm2.bias, self.norm2.eps, xn)
         w, b = pack_linear(self.mlp.fc1)
         hid = ws.buf("blk_h", M, w.shape[0], torch.bfloat16)
+        yield_point()
         N.gemm_bf16(xn, w, b, hid, N.EPI_GELU_BF16)
         w, b = pack_linear(self.mlp.fc2)
         # the row pass has kernels for C / 256 in {1, 2, 4, 8} only (norm.hip)
