@@ -14,3 +14,5 @@ timeout -k 10 300 python -u bench.py > "$OUT/bench.out" 2> "$OUT/bench.err" || e
 grep '^{' "$OUT/bench.out" | tail -1 | cut -c1-300
 timeout -k 10 400 python -u bench.py --config 3 --steps 3 --warmup 2 --no-cpu-baseline > "$OUT/c3.out" 2> "$OUT/c3.err" || exit 1
 grep '^{' "$OUT/c3.out" | tail -1 | cut -c1-200
+timeout -k 10 300 python -u bench.py --config 0 --steps 10 --warmup 3 > "$OUT/c0.out" 2> "$OUT/c0.err" || exit 1
+grep '^{' "$OUT/c0.out" | tail -1 | cut -c1-200
