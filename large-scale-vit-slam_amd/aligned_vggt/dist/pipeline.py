@@ -518,12 +518,14 @@ class ChunkPipeline:
                     ctx = self._ctx_from(ctx_in, B, memory_shape)
                 if gate is not None:
                     gate.begin(side)  # the encode stream pauses at its next yield point
-                ev0 = self._tick()
-                pred = self.model.align_chunk(enc, num_overlap, ctx)
-                if ev0 is not None:
-                    self.align_events.append((i, ev0, self._tick()))
-                if gate is not None:
-                    gate.end(side)
+                try:
+                    ev0 = self._tick()
+                    pred = self.model.align_chunk(enc, num_overlap, ctx)
+                    if ev0 is not None:
+                        self.align_events.append((i, ev0, self._tick()))
+                finally:
+                    if gate is not None:
+                        gate.end(side)  # also on an error: a held gate would stall every later encode
                 if i + 1 < n:
                     if W > 1:
                         sends.append(self._isend(pred, (i + 1) % W, keys))
