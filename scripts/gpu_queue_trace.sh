@@ -2,7 +2,7 @@
 # kernel trace of the overlapped configs[3] schedule (W = 1 ring, short-workgroup streams): per-queue busy / gaps
 set -u
 cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-T=${1:-r8o}
+T=${1:-queue_trace}
 OUT=gpurun_out/$T
 mkdir -p "$OUT"
 export TMPDIR=/tmp
