@@ -1,5 +1,5 @@
 #!/bin/bash
-# kernel trace of the overlapped configs[3] schedule (W = 1 ring, short-workgroup streams): per-queue busy / gaps
+# kernel trace of the overlapped configs[3] schedule (W = 1 ring with the default gated encode): per-queue busy / gaps
 set -u
 cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 T=${1:-queue_trace}
