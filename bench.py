@@ -339,8 +339,15 @@ def main():
                          "unit": "TFLOP/s",
                          "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4) if attn_tflops else None,
                          "avg_launch_ms": round(attn_ms, 4) if attn_ms else None,
-                         "flops_per_launch": fl["global_attn_launch"], "traffic": _pmc_traffic()},
+                         "flops_per_launch": fl["global_attn_launch"], "traffic": _pmc_traffic(),
+                         "traffic_provenance": _counter_provenance("attn_traffic.json")},
+            "mfma_util_pmc_provenance": _counter_provenance("step_mfma.json"),
         }
+        if os.environ.get("VGGT_MFMA_PROBE", "1") != "0":
+            # the peak the roofline is priced against, measured on this device after the timed
+            # region: back-to-back 32x32x16 bf16 MFMAs, sustained TF/s + clock
+            line["mfma_peak_measured"] = {"random_operands": _native.mfma_probe(random=True),
+                                          "zero_operands": _native.mfma_probe(random=False)}
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(args.cpu_threads)
         print(json.dumps(line), flush=True)
@@ -353,12 +360,35 @@ def _pmc_traffic():
     (profiles/attn_traffic.json, written by scripts/pmc_traffic.py from two
     separate `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` passes of this
     same bench command; FETCH_SIZE x2 per the gfx950 correction), or None."""
-    p = os.path.join(ROOT, "profiles", "attn_traffic.json")
+    d = _committed_counters("attn_traffic.json")
+    return None if d is None else d.get("hbm_bytes_per_launch")
+
+
+def _committed_counters(name: str):
+    """A committed counter file (profiles/<name>) if it was measured on these
+    sources (aligned_vggt.provenance: same source fingerprint), else None --
+    a stale counter is never reported as current."""
+    from aligned_vggt.provenance import source_fingerprint
     try:
-        with open(p) as fh:
-            return json.load(fh)["hbm_bytes_per_launch"]
-    except (OSError, ValueError, KeyError):
+        with open(os.path.join(ROOT, "profiles", name)) as fh:
+            d = json.load(fh)
+    except (OSError, ValueError):
         return None
+    if d.get("source_fingerprint") != source_fingerprint():
+        return None
+    return d
+
+
+def _counter_provenance(name: str) -> dict:
+    try:
+        with open(os.path.join(ROOT, "profiles", name)) as fh:
+            d = json.load(fh)
+    except (OSError, ValueError):
+        return {"file": "profiles/" + name, "status": "missing"}
+    from aligned_vggt.provenance import source_fingerprint
+    fp = source_fingerprint()
+    return {"file": "profiles/" + name, "git_head": d.get("git_head"), "source_fingerprint": d.get("source_fingerprint"),
+            "status": "current" if d.get("source_fingerprint") == fp else "stale (measured on other sources: not used)"}
 
 
 def _step_pmc():
@@ -366,14 +396,11 @@ def _step_pmc():
     summary (profiles/step_mfma.json, scripts/gpu_step_pmc.sh: rocprofv3 --pmc
     SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE over one step of this bench,
     and SQ_INSTS_VALU_MFMA_MOPS_BF16), or None."""
-    p = os.path.join(ROOT, "profiles", "step_mfma.json")
-    try:
-        with open(p) as fh:
-            d = json.load(fh)
-    except (OSError, ValueError):
+    d = _committed_counters("step_mfma.json")
+    if d is None:
         return None
     out = {"mfma_busy_frac": d.get("mfma_busy_frac"), "by_class": d.get("mfma_busy_frac_by_class"),
-           "source": "profiles/step_mfma.json"}
+           "source": "profiles/step_mfma.json", "git_head": d.get("git_head")}
     if d.get("mfma_bf16_tflop_counted") is not None:
         out["bf16_tflop_counted_per_step"] = round(d["mfma_bf16_tflop_counted"], 3)
     return out
@@ -430,9 +457,11 @@ def bench_full(args, world, rank, dev):
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
-    recurrence = None
+    recurrence = ring_model = None
     if args.workload == "sequence" and os.environ.get("VGGT_RECURRENCE_PROBE", "1") != "0":
         recurrence = _recurrence_probe(pipe, step, n_chunks_step, dt / args.steps * 1e3, world)
+        if world == 1:
+            ring_model = _ring_model(model, pipe, seq, S, ov, recurrence, dt / args.steps * 1e3)
     if world > 1:
         dist.destroy_process_group()
     if rank == 0:
@@ -449,7 +478,7 @@ def bench_full(args, world, rank, dev):
                                             "parallelism": ("chunk pipeline x%d (RCCL baton ring)" % world
                                                             if args.workload == "sequence" else
                                                             "replicas x%d" % world)},
-            "recurrence": recurrence}),
+            "recurrence": recurrence, "ring_model": ring_model}),
               flush=True)
 
 
@@ -466,7 +495,7 @@ def _recurrence_probe(pipe, step, n_chunks, t1_ms, world):
     ring's defaults (the encode gated while an alignment runs, persistent
     GEMMs), gated with short-workgroup streams, ungated short-workgroup, ungated
     persistent (the round-3 schedule) and, for VGGT_PROBE_RESERVE=r,..., with
-    the encodes masked off r CUs.  bound_frac_* =
+    the encodes masked off r CUs.  chain_lower_bound_frac_* (a lower bound only) =
     n_chunks x t_align over the overlapped sequence time / 8: the 8-rank ring's
     critical path against its encode share (<= 1: the encodes bound it)."""
     import statistics
@@ -489,12 +518,15 @@ def _recurrence_probe(pipe, step, n_chunks, t1_ms, world):
             pipe.short_workgroups = short
         if gate is not None:
             pipe.gate_encode = gate
+        keep_gates = pipe.plan_gates
+        pipe.plan_gates = (pipe.gate_encode,)  # the mode's gate on every rank, not the planner's choice
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         step()
         torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) * 1e3
         pipe.overlap_align, pipe.reserve_cus, pipe.short_workgroups, pipe.gate_encode = keep
+        pipe.plan_gates = keep_gates
         ms = pipe.align_ms()
         out["t_align_ms_%s_median" % name] = round(statistics.median(ms), 3) if ms else None
         out["t_align_ms_%s_max" % name] = round(max(ms), 3) if ms else None
@@ -502,16 +534,86 @@ def _recurrence_probe(pipe, step, n_chunks, t1_ms, world):
     pipe.time_align = False
     t_load = out.get("t_align_ms_under_load_median")
     if t_load and world == 1:
-        out["T8_lower_bound_ms"] = round(n_chunks * t_load, 1)
+        # a LOWER BOUND only: the recurrence alone (n_chunks x t_align), ignoring the
+        # pipeline fill, each rank's encode work and the baton hops -- ring_model is the
+        # prediction of the 8-rank sequence time
+        out["T8_chain_lower_bound_ms"] = round(n_chunks * t_load, 1)
         out["T1_over_8_ms"] = round(t1_ms / 8, 1)
-        out["bound_frac_of_T1_over_8"] = round(n_chunks * t_load / (t1_ms / 8), 3)
-        # the same bound against the encode time of that configuration (the W = 1
-        # overlapped sequence on its encode stream, / 8)
+        out["chain_lower_bound_frac_of_T1_over_8"] = round(n_chunks * t_load / (t1_ms / 8), 3)
         for name, ov_mode, r, _, _ in modes:
             t = out.get("t_align_ms_%s_median" % name)
             if ov_mode and t:
-                out["bound_frac_%s" % name] = round(n_chunks * t / (out["sequence_ms_%s" % name] / 8), 3)
+                out["chain_lower_bound_frac_%s" % name] = round(n_chunks * t / (out["sequence_ms_%s" % name] / 8), 3)
     return out
+
+
+def _ring_model(model, pipe, seq, S, ov, rec, t1_ms):
+    """The W-rank ring's sequence time predicted by the discrete-event model
+    of aligned_vggt/dist/schedule.py from costs measured here on one GPU:
+    core / dense encode jobs of g = 1..cap chunks (and the tail chunk), HIP
+    events on one stream, median of 3 after a warm-up; t_align alone / beside
+    a gated encode / ungated from the recurrence probe; the encode time one
+    alignment costs its rank (t_pause) from the W = 1 overlapped sequences
+    minus their plan's job time.  The baton hop (28 MB over one xGMI link) is
+    not measurable on one GPU: 0.25 ms is modelled.  T1 = this run's
+    measured single-rank sequence."""
+    import statistics
+    from aligned_vggt.dist import schedule as SC
+    from aligned_vggt.utils.data import generate_chunks
+    chunks = generate_chunks(seq.shape[1], "chunk_overlap", S, ov)
+    lengths = [len(c) for c in chunks]
+    cap = pipe._group_cap(chunks, seq)
+    cur = torch.cuda.current_stream()
+
+    def timed(fn, reps=3):
+        fn()
+        ts = []
+        for _ in range(reps):
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record(cur)
+            r = fn()
+            b.record(cur)
+            b.synchronize()
+            ts.append(a.elapsed_time(b))
+        return statistics.median(ts), r
+
+    core, dense = {}, {}
+    shapes = [(lengths[0], g) for g in range(1, cap + 1)]
+    if lengths[-1] != lengths[0]:
+        shapes.append((lengths[-1], 1))
+    with torch.no_grad():
+        for fr, g in shapes:
+            idx = [i for i, c in enumerate(chunks) if len(c) == fr][:g]
+            x = torch.cat([seq[:, chunks[i]] for i in idx], 0)
+            core[(fr, g)], enc = timed(lambda: model.encode_chunk(x, dense=False))
+            dense[(fr, g)], _ = timed(lambda: model.encode_dense(dict(enc)))
+            del enc
+    costs = SC.RingCosts(core={k: round(v, 3) for k, v in core.items()},
+                         dense={k: round(v, 3) for k, v in dense.items()},
+                         t_align=rec["t_align_ms_under_load_median"] or 0.0,
+                         t_align_alone=rec["t_align_ms_alone_median"] or 0.0, t_pause=0.0,
+                         t_align_ungated=rec["t_align_ms_under_load_ungated_median"] or 0.0,
+                         source="bench.py --workload sequence on one MI355X (this line)")
+    # t_pause: what the overlapped W = 1 sequences spent beyond their plans' job time, per alignment
+    n = len(lengths)
+    for gated, seq_key in ((True, "sequence_ms_under_load"), (False, "sequence_ms_under_load_ungated")):
+        plans, _ = SC.plan_ring(lengths, 1, costs, cap, pipe.plan_policies, (gated,))
+        jobs_ms = sum(costs.job_ms(k, lengths[g[0]], len(g)) for k, g in plans[0].jobs)
+        tp = max(0.0, (rec[seq_key] - costs.gather - jobs_ms) / n)
+        if gated:
+            costs.t_pause = round(tp, 3)
+        else:
+            costs.t_pause_ungated = round(tp, 3)
+    pred = SC.predict_scaling(lengths, costs)
+    for W, d in pred.items():
+        d["T1_over_TW"] = round(t1_ms / d["T_ms"], 2)
+    w1, _ = SC.plan_ring(lengths, 1, costs, cap, pipe.plan_policies, (True,))
+    return {"costs": costs.to_json(), "T1_measured_ms": round(t1_ms, 1), "predicted": pred,
+            "check_w1_overlapped_gated": {"predicted_ms": round(SC.simulate(lengths, 1, w1, costs).total_ms, 1),
+                                          "measured_ms": rec["sequence_ms_under_load"],
+                                          "note": "t_pause is calibrated on this run, so this agrees by construction "
+                                                  "up to the plan and alone-time terms"}}
 
 
 def bench_point(args, world, rank, dev):

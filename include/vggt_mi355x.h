@@ -559,6 +559,12 @@ size_t vggt_batch_dot_workspace_bytes(int B, int64_t n);
 int vggt_batch_dot_f32(const float* a, const float* c, int64_t bs, int B, int64_t n, float* out, void* ws,
                        size_t ws_bytes, void* stream);
 
+/* MFMA peak probe (diagnostic; BASELINE.md §2 asks for a measured MFMA microbenchmark with its clock):
+ * nwg workgroups of 4 waves issue iters x 8 v_mfma_f32_32x32x16_bf16 each on the bf16 operands
+ * (nwg * 256 * 16 elements: random or zeros), 32768 FLOP per MFMA; stamps[4 * wg] = s_memtime before /
+ * after the loop, s_memrealtime (100 MHz) before / after.  sink: nwg * 256 floats, never read. */
+int vggt_mfma_probe(unsigned long long* stamps, float* sink, const void* operands, int nwg, int iters, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

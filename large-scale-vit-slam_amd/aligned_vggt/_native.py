@@ -30,6 +30,7 @@ _vp, _i, _i64, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_floa
 _SIGS = {
     "vggt_tune": [_i, _i],
     "vggt_set_stream_config": [_vp, _i, _i],
+    "vggt_mfma_probe": [_vp, _vp, _vp, _i, _i, _vp],
     "vggt_gemm_bf16": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _vp, _i64, _vp, _vp, _i64, _vp],
     "vggt_gemm_qkv": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _vp, _i64, _vp, _vp, _vp, _vp, _f, _i, _vp, _i, _vp,
                       _vp, _i, _vp],
@@ -161,6 +162,44 @@ def set_stream_config(stream: int, cus: int, flags: int = 0) -> int:
     if rc < 0:
         raise ValueError(f"vggt_set_stream_config: rejected ({rc})")
     return rc
+
+
+def mfma_probe(iters: int = 200_000, random: bool = True, seconds: float = 2.0, device=None) -> dict:
+    """Sustained bf16 MFMA rate and in-kernel clock (vggt_mfma_probe): one
+    workgroup of 4 waves per CU, back-to-back launches for ``seconds`` (the
+    clock the chip holds under load), the last launch timed by HIP events and
+    stamped with s_memtime / s_memrealtime; returns TF/s, the clock (median over
+    workgroups) and the FLOP per cycle per CU that implies."""
+    import statistics
+    device = torch.device(device or "cuda")
+    ncu = torch.cuda.get_device_properties(device).multi_processor_count
+    g = torch.Generator(device="cpu").manual_seed(0)
+    n = ncu * 256 * 16
+    ops = (torch.randn(n, generator=g) if random else torch.zeros(n)).to(torch.bfloat16).to(device)
+    stamps = torch.zeros(ncu * 4, dtype=torch.int64, device=device)
+    sink = torch.empty(ncu * 256, dtype=torch.float32, device=device)
+    st = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    launch = lambda: _check(lib().vggt_mfma_probe(_p(stamps), _p(sink), _p(ops), ncu, iters, st),  # noqa: E731
+                            "vggt_mfma_probe")
+    import time
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end:
+        launch()
+        torch.cuda.synchronize(device)
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    a.record()
+    launch()
+    b.record()
+    b.synchronize()
+    ms = a.elapsed_time(b)
+    sp = stamps.view(ncu, 4).cpu().tolist()
+    clocks = [(t1 - t0) / (r1 - r0) * 100e6 for t0, t1, r0, r1 in sp if r1 > r0]
+    clk = statistics.median(clocks)
+    flop = ncu * 4 * iters * 8 * 32768.0
+    return {"tflops": round(flop / (ms * 1e-3) / 1e12, 1), "clock_ghz": round(clk / 1e9, 3),
+            "flop_per_cycle_per_cu": round(flop / ncu / (ms * 1e-3 * clk), 1), "ms": round(ms, 3), "cus": ncu,
+            "operands": "random bf16" if random else "zeros"}
 
 
 def _check(rc: int, name: str) -> None:

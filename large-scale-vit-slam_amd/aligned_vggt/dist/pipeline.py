@@ -208,6 +208,39 @@ class ChunkPipeline:
         if encode_group is None:
             encode_group = int(os.environ.get("VGGT_ENCODE_GROUP", "3"))
         self.encode_group = max(1, encode_group)
+        # the ring's planner (dist/schedule.py) may choose, per rank, where the DPT heads
+        # run ("with" the encode, "lag" one group behind, at the "end") and whether the
+        # rank's encode is gated; these restrict its choices
+        self.plan_policies = tuple(os.environ.get("VGGT_RING_POLICIES", "with,lag,end").split(","))
+        self.plan_gates = (True, False)
+        self._local = None
+        self.prediction = None
+
+    # ------------------------------------------------------------ lifetime
+    def close(self) -> None:
+        """Release what the pipeline created on the device: the encode gate's
+        signal word, the library's per-stream configuration slots and the
+        dedicated HIP streams."""
+        from ..runtime import destroy_stream
+        gate = self.__dict__.pop("_gate", None)
+        if gate is not None:
+            gate.close()
+        owned = self.__dict__.pop("_owned_streams", [])
+        if owned:
+            from .. import _native as N
+            torch.cuda.synchronize(self.device)
+            for s in owned:
+                N.set_stream_config(s.cuda_stream, 0, 0)  # frees the slot (capi.cpp)
+                destroy_stream(s)
+        self.__dict__.pop("_enc_streams", None)
+        self.__dict__.pop("_align_streams", None)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
 
     # ----------------------------------------------------- frame transfer
     def _fetch(self, images: torch.Tensor, idx):
@@ -301,7 +334,6 @@ class ChunkPipeline:
         on every rank (pose_enc (B,N,9), chunk_sim3_alignment_enc (B,n_chunks,8),
         frame_se3_alignment_enc (B,sum(S_i-1),7), and depth if gathered)."""
         B, Nf = images.shape[:2]
-        self._img_hw = tuple(images.shape[-2:])
         chunks = generate_chunks(Nf, "chunk_overlap", chunk_width, num_overlap)
         keys = ["overlap_tokens", "pose_enc"] + (["memory_tokens"] if memory_shape is not None else [])
         self.align_events = []
@@ -343,6 +375,7 @@ class ChunkPipeline:
                 s = dedicated_stream(self.device)
             N.set_stream_config(s.cuda_stream, cus, N.STREAM_SHORT_WORKGROUPS if self.short_workgroups else 0)
             streams[key] = s
+            self.__dict__.setdefault("_owned_streams", []).append(s)
         return s
 
     def _groups(self, chunks, own: List[int], images) -> List[List[int]]:
@@ -350,12 +383,54 @@ class ChunkPipeline:
         g = _encode_groups([len(chunks[i]) for i in own], images, self.model, self.encode_group)
         return [[own[j] for j in grp] for grp in g]
 
-    def _encode(self, images, chunks, g: List[int], frames) -> Dict[int, dict]:
+    def _group_cap(self, chunks, images) -> int:
+        """Most chunks one encode may batch (encode_group, GROUP_TOKENS token rows)."""
+        B, H, W = images.shape[0], images.shape[-2], images.shape[-1]
+        agg = getattr(self.model, "aggregator", None)
+        ps = getattr(agg, "patch_size", 14)
+        ps = ps[0] if isinstance(ps, (tuple, list)) else int(ps)
+        P = (H // ps) * (W // ps) + int(getattr(agg, "patch_start_idx", 5))
+        n = max(len(c) for c in chunks)
+        return max(1, min(self.encode_group, GROUP_TOKENS // (B * n * P)))
+
+    def plans(self, chunks, images, cuda: bool):
+        """This ring's per-rank encode plans (dist/schedule.py ``plan_ring``:
+        group sizes, where the DPT heads run, gated or not; cached per
+        chunking).  VGGT_RING_PLAN=legacy: round 4's schedule (greedy groups of
+        the cap, DPT inside each encode, every rank gated) for A/B."""
+        from . import schedule as SC
+        W = self.world
+        lengths = [len(c) for c in chunks]
+        cap = self._group_cap(chunks, images)
+        defer = hasattr(self.model, "encode_dense") and getattr(self.model, "point_head", None) is None
+        policies = tuple(self.plan_policies) if defer else ("with",)
+        gates = tuple(self.plan_gates) if (cuda and self.gate_encode) else (False,)
+        legacy = os.environ.get("VGGT_RING_PLAN", "auto") == "legacy"
+        key = (tuple(lengths), W, cap, policies, gates, legacy)
+        cache = self.__dict__.setdefault("_plan_cache", {})
+        if key not in cache:
+            costs = SC.load_costs()
+            if legacy:
+                plans = SC.legacy_plans(lengths, W, cap)
+                for pl in plans:
+                    pl.gated = gates[0]
+                pred = SC.simulate(lengths, W, plans, costs)
+            else:
+                plans, pred = SC.plan_ring(lengths, W, costs, cap, policies, gates)
+            cache[key] = (plans, pred)
+        self.prediction = cache[key][1]
+        return cache[key][0]
+
+    def _encode(self, images, chunks, g: List[int], frames, dense: bool = True):
+        """One encode job over the chunks in g: (per-chunk results, the batched result)."""
         xs = [self._ready(f) for f in frames]
         B = xs[0].shape[0]
+        kw = {} if dense else {"dense": False}
         if len(g) == 1:
-            return {g[0]: self.model.encode_chunk(xs[0])}
-        return dict(zip(g, _split_batch(self.model.encode_chunk(torch.cat(xs, 0)), B, len(g))))
+            enc = self.model.encode_chunk(xs[0], **kw)
+            return {g[0]: enc}, enc
+        enc = self.model.encode_chunk(torch.cat(xs, 0), **kw)
+        return dict(zip(g, _split_batch(enc, B, len(g)))), enc
 
     @staticmethod
     def _summary(pred: dict, S: int) -> dict:
@@ -391,7 +466,7 @@ class ChunkPipeline:
                 frames, g = nxt, groups[gi]
                 gi += 1
                 nxt = fetch(groups[gi]) if gi < len(groups) else None
-                encs.update(self._encode(images, chunks, g, frames))
+                encs.update(self._encode(images, chunks, g, frames)[0])
             ctx = self._ctx_from(local, B, memory_shape) if i > 0 else None
             ev0 = self._tick()
             pred = self.model.align_chunk(encs.pop(i), num_overlap, ctx)
@@ -402,13 +477,50 @@ class ChunkPipeline:
             mine[i] = self._summary(pred, len(chunks[i]))
         return mine
 
+    def _align_stream(self, align_short: bool):
+        """The high-priority stream alignments run on (cached)."""
+        streams = self.__dict__.setdefault("_align_streams", {})
+        side = streams.get(align_short)
+        if side is None:
+            lo, hi = torch.cuda.Stream.priority_range()
+            if align_short:
+                # a dedicated high-priority stream, also short-workgroup: beside an encode its
+                # GEMMs' tiles go to whichever CUs free up first instead of one persistent
+                # workgroup per CU that starts only when its CU does
+                from .. import _native as N
+                from ..runtime import dedicated_stream
+                side = dedicated_stream(self.device, priority=hi)
+                N.set_stream_config(side.cuda_stream, 0, N.STREAM_SHORT_WORKGROUPS)
+                self.__dict__.setdefault("_owned_streams", []).append(side)
+            else:
+                side = torch.cuda.Stream(self.device, priority=hi)
+            streams[align_short] = side
+        return side
+
+    def _gate_for(self, main, side, plan) -> object:
+        """The encode gate of this rank, or None.  Only when the alignment
+        stream outranks the encode stream: a gated wait then never sits in a
+        hardware queue ahead of the alignment's end() write (runtime.EncodeGate)."""
+        if not (self.gate_encode and plan.gated and main.cuda_stream != 0):
+            return None
+        from ..runtime import EncodeGate, stream_priority
+        if not stream_priority(side) < stream_priority(main):
+            return None
+        gate = self.__dict__.get("_gate")
+        if gate is None:
+            gate = self._gate = EncodeGate(self.device)
+        return gate
+
     def _run_ring(self, images, chunks, num_overlap, keys, token_dims, memory_shape, B) -> Dict[int, dict]:
-        """Rank r owns chunks r, r + W, ...  Encodes run on the compute stream
-        one group ahead; each alignment runs on a high-priority side stream
-        that waits (device-side) for its encode and for the baton from rank
-        i - 1, and posts the baton to rank i + 1 (isend) as soon as it is
-        done -- the host never blocks on a peer, and the compute stream keeps
-        encoding while a baton is in flight.
+        """Rank r owns chunks r, r + W, ...  Its encode stream runs the plan's
+        jobs (dist/schedule.py: groups of its own chunks, the DPT heads with
+        the encode or later); each alignment runs on a high-priority side
+        stream that waits (device-side) for its chunk's core encode and for the
+        baton from rank i - 1, and posts the baton to rank i + 1 (isend) as
+        soon as it is done -- the host never blocks on a peer, and the compute
+        stream keeps encoding while a baton is in flight.  Depth maps whose
+        DPT head ran after the alignment are scaled by the chunk Sim(3) at the
+        end (``scale_dense``).
 
         The baton's irecv is posted on the side stream BEFORE the side stream
         waits for the chunk's encode: RCCL orders its communication stream
@@ -419,48 +531,43 @@ class ChunkPipeline:
 
         W == 1 (``overlap_align``): the same schedule on one GPU with the baton
         kept on the device -- chunk i aligns on the side stream while the next
-        encode group runs on the compute stream."""
+        encode job runs on the compute stream."""
+        from .schedule import enqueue_order
         W, r = self.world, self.rank
         n = len(chunks)
         P1, C = token_dims
         cuda = self.device is not None and torch.device(self.device).type == "cuda"
         self._p2p_warmup()
         own = list(range(r, n, W))
-        groups = self._groups(chunks, own, images)
-        group_of = {i: gi for gi, g in enumerate(groups) for i in g}
-        side = None
+        plan = self.plans(chunks, images, cuda)[r]
+        self.enqueue_log = []  # ("job", kind, chunks) / ("align", i): the host's issue order (tests)
+        side = main = None
         if cuda:
             # the alignment's own GEMMs: persistent when the encode is gated (the
             # alignment then has the GPU to itself after one yield interval), else short
-            align_short = self.short_workgroups and not self.gate_encode
-            streams = self.__dict__.setdefault("_align_streams", {})
-            side = streams.get(align_short)
-            if side is None:
-                lo, hi = torch.cuda.Stream.priority_range()
-                if align_short:
-                    # a dedicated high-priority stream, also short-workgroup: beside an encode its
-                    # GEMMs' tiles go to whichever CUs free up first instead of one persistent
-                    # workgroup per CU that starts only when its CU does
-                    from .. import _native as N
-                    from ..runtime import dedicated_stream
-                    side = dedicated_stream(self.device, priority=hi)
-                    N.set_stream_config(side.cuda_stream, 0, N.STREAM_SHORT_WORKGROUPS)
-                else:
-                    side = torch.cuda.Stream(self.device, priority=hi)
-                streams[align_short] = side
-        main = torch.cuda.current_stream(self.device) if cuda else None
-        gate = None
-        if cuda and self.gate_encode and main.cuda_stream != 0:
-            from ..runtime import EncodeGate
-            gate = self.__dict__.get("_gate")
-            if gate is None:
-                gate = self._gate = EncodeGate(self.device)
+            side = self._align_stream(self.short_workgroups and not (self.gate_encode and plan.gated))
+            main = torch.cuda.current_stream(self.device)
+        gate = self._gate_for(main, side, plan) if cuda else None
         encs: Dict[int, dict] = {}
         ready: Dict[int, object] = {}
+        held: Dict[tuple, dict] = {}  # batched core results waiting for their DPT job
+        dense: Dict[int, dict] = {}
 
-        def enqueue(gi):
-            g = groups[gi]
-            out = self._encode(images, chunks, g, [self._fetch(images, chunks[i]) for i in g])
+        def run_job(j):
+            kind, g = plan.jobs[j]
+            self.enqueue_log.append(("job", kind, tuple(g)))
+            if kind == "dense":
+                benc = held.pop(tuple(g))
+                self.model.encode_dense(benc)
+                dk = {k: benc[k] for k in ("depth", "depth_conf") if k in benc}
+                parts = [dk] if len(g) == 1 else _split_batch(dk, benc["images"].shape[0] // len(g), len(g))
+                for i, p in zip(g, parts):
+                    dense[i] = p
+                return
+            out, benc = self._encode(images, chunks, list(g), [self._fetch(images, chunks[i]) for i in g],
+                                     dense=(kind == "enc"))
+            if kind == "core":
+                held[tuple(g)] = benc
             ev = None
             if cuda:
                 ev = torch.cuda.Event()
@@ -476,8 +583,13 @@ class ChunkPipeline:
             from ..runtime import gated
             gate_ctx = gated(main, gate)
         with gate_ctx:
-            self._ring_loop(own, group_of, groups, enqueue, encs, ready, side, cuda, chunks, num_overlap, keys,
-                            B, P1, C, memory_shape, mine, sends, gate)
+            for kind, arg in enqueue_order(plan, own):
+                if kind == "job":
+                    run_job(arg)
+                else:
+                    self.enqueue_log.append(("align", arg[0]))
+                    self._align_one(arg[0], encs, ready, side, cuda, chunks, num_overlap, keys, B, P1, C,
+                                    memory_shape, mine, sends, gate)
         for works, _ in sends:
             for w in works:
                 w.wait()
@@ -485,53 +597,53 @@ class ChunkPipeline:
             main.wait_stream(side)
             for v in mine.values():
                 _record_stream(v, main)
+        for i, d in dense.items():  # featureAligned_vggt.py:171 for the deferred depth maps
+            mine[i].update(self.model.scale_dense(d, mine[i]["chunk_sim3"]))
         return mine
 
-    def _ring_loop(self, own, group_of, groups, enqueue, encs, ready, side, cuda, chunks, num_overlap, keys,
-                   B, P1, C, memory_shape, mine, sends, gate) -> None:
+    def _align_one(self, i, encs, ready, side, cuda, chunks, num_overlap, keys, B, P1, C, memory_shape, mine,
+                   sends, gate) -> None:
         W, n = self.world, len(chunks)
-        local = None
-        enqueued = 0
-        for i in own:
-            gi = group_of[i]
-            while enqueued <= min(gi + 1, len(groups) - 1):  # this group and the next one queued
-                enqueue(enqueued)
-                enqueued += 1
-            enc = encs.pop(i)
-            with (torch.cuda.stream(side) if cuda else contextlib.nullcontext()):
-                ctx = None
-                works = ()
-                if i > 0 and W > 1:
-                    Sp = len(chunks[i - 1])
-                    works, ctx_in = self._irecv((i - 1) % W, self._baton_shapes(
-                        B, Sp, _overlap_of(Sp, num_overlap), P1, C, memory_shape))
-                if cuda:
-                    side.wait_event(ready.pop(i))
-                    _record_stream(enc, side)
-                if i > 0:
-                    if W > 1:
-                        for w in works:
-                            w.wait()  # RCCL: the side stream waits; gloo: the host does
-                        ctx_in = {k: v.to(self.device) for k, v in ctx_in.items()}  # no-op unless host-staged
-                    else:
-                        ctx_in = local
-                    ctx = self._ctx_from(ctx_in, B, memory_shape)
+        enc = encs.pop(i)
+        with (torch.cuda.stream(side) if cuda else contextlib.nullcontext()):
+            ctx = None
+            works = ()
+            if i > 0 and W > 1:
+                Sp = len(chunks[i - 1])
+                works, ctx_in = self._irecv((i - 1) % W, self._baton_shapes(
+                    B, Sp, _overlap_of(Sp, num_overlap), P1, C, memory_shape))
+            if cuda:
+                side.wait_event(ready.pop(i))
+                _record_stream(enc, side)
+            if i > 0:
+                if W > 1:
+                    for w in works:
+                        w.wait()  # RCCL: the side stream waits; gloo: the host does
+                    ctx_in = {k: v.to(self.device) for k, v in ctx_in.items()}  # no-op unless host-staged
+                else:
+                    ctx_in = self._local
+                ctx = self._ctx_from(ctx_in, B, memory_shape)
+            if gate is not None and hasattr(self.model, "prepare_align"):
+                # whatever may synchronise the device (a HIP graph's first capture) happens
+                # BEFORE the gate closes: a device-wide wait while it is held would wait for
+                # the paused encode, which waits for the gate (runtime.EncodeGate)
+                self.model.prepare_align(enc, num_overlap, ctx)
+            if gate is not None:
+                gate.begin(side)  # the encode stream pauses at its next yield point
+            try:
+                ev0 = self._tick()
+                pred = self.model.align_chunk(enc, num_overlap, ctx)
+                if ev0 is not None:
+                    self.align_events.append((i, ev0, self._tick()))
+            finally:
                 if gate is not None:
-                    gate.begin(side)  # the encode stream pauses at its next yield point
-                try:
-                    ev0 = self._tick()
-                    pred = self.model.align_chunk(enc, num_overlap, ctx)
-                    if ev0 is not None:
-                        self.align_events.append((i, ev0, self._tick()))
-                finally:
-                    if gate is not None:
-                        gate.end(side)  # also on an error: a held gate would stall every later encode
-                if i + 1 < n:
-                    if W > 1:
-                        sends.append(self._isend(pred, (i + 1) % W, keys))
-                    else:
-                        local = {k: (pred[k][-1] if isinstance(pred[k], list) else pred[k]) for k in keys}
-                mine[i] = self._summary(pred, len(chunks[i]))
+                    gate.end(side)  # also on an error: a held gate would stall every later encode
+            if i + 1 < n:
+                if W > 1:
+                    sends.append(self._isend(pred, (i + 1) % W, keys))
+                else:
+                    self._local = {k: (pred[k][-1] if isinstance(pred[k], list) else pred[k]) for k in keys}
+            mine[i] = self._summary(pred, len(chunks[i]))
 
     def _tick(self):
         """A timing event on the current stream (``time_align`` on a HIP device), else None."""
@@ -579,8 +691,9 @@ class ChunkPipeline:
         slots = (n + W - 1) // W
         smax = max(len(c) for c in chunks)
         dev = self._comm_device
-        # small outputs, per slot: [has_depth, pose_enc B*smax*9, chunk_sim3 B*8, frame_se3 B*(smax-1)*7]
-        seg = (1, B * smax * 9, B * 8, B * (smax - 1) * 7)
+        # small outputs, per slot: [has_depth, depth H, depth W, pose_enc B*smax*9, chunk_sim3 B*8,
+        # frame_se3 B*(smax-1)*7]; the DPT maps are 14*(H//14) x 14*(W//14), so their size travels too
+        seg = (3, B * smax * 9, B * 8, B * (smax - 1) * 7)
         per = sum(seg)
         buf = torch.zeros(slots, per, device=dev, dtype=torch.float32)
         for j in range(slots):
@@ -589,7 +702,9 @@ class ChunkPipeline:
                 continue
             S, m = len(chunks[i]), mine[i]
             o = seg[0]
-            buf[j, 0] = float(self.gather_dense and "depth" in m)
+            if self.gather_dense and "depth" in m:
+                buf[j, 0] = 1.0
+                buf[j, 1], buf[j, 2] = float(m["depth"].shape[2]), float(m["depth"].shape[3])
             buf[j, o:o + B * S * 9] = m["pose_enc"].reshape(-1).to(dev)
             o += seg[1]
             buf[j, o:o + B * 8] = m["chunk_sim3"].reshape(-1).to(dev)
@@ -610,8 +725,10 @@ class ChunkPipeline:
             o += seg[2]
             per_chunk[i]["frame_se3"] = row[o:o + B * (S - 1) * 7].view(B, S - 1, 7)
         # every rank sees every chunk's flag, so all agree on the dense collective
-        if bool((allb[:, 0] > 0).any()) and all(float(allb[(i % W) * slots + i // W, 0]) > 0 for i in range(n)):
-            H, Wd = self._img_hw
+        # (one device-to-host copy of the flag column)
+        flags = allb[:, :3].cpu()
+        if all(float(flags[(i % W) * slots + i // W, 0]) > 0 for i in range(n)):
+            H, Wd = int(flags[0, 1]), int(flags[0, 2])  # chunk 0 = rank 0's slot 0
             pix = H * Wd
             d = torch.zeros(slots, 2, B * smax * pix, device=dev, dtype=torch.float32)
             for j in range(slots):

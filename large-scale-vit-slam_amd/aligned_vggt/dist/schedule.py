@@ -1,0 +1,374 @@
+"""Per-rank encode plans for the chunk pipeline's baton ring, and the
+discrete-event model that picks them.
+
+The reference runs its chunks strictly one after another
+(training_metrics.py:643-652; featureAligned_vggt.py:84-94 threads
+``context`` chunk to chunk).  ``ChunkPipeline`` splits each chunk's forward
+into context-free encode work and the recurrent ``align_chunk``; chunk i is
+owned by rank i mod W.  A rank's encode stream runs *jobs*:
+
+  * ``("enc", g)``   aggregator + camera head + alignment prefix + DPT heads of
+    the chunks in ``g`` as one batch (``encode_chunk``);
+  * ``("core", g)``  the same without the DPT heads -- everything the
+    alignment recurrence needs (``encode_chunk(..., dense=False)``);
+  * ``("dense", g)`` the DPT heads of a group whose core ran earlier
+    (``encode_dense``); its outputs are scaled by the chunk Sim(3) after the
+    alignment (featureAligned_vggt.py:171) at the end of the sequence.
+
+Alignment i runs on rank i mod W when chunk i's core is done and alignment
+i-1 has finished on the previous rank (+ one baton hop); while it runs, the
+rank's encode stream is paused by the encode gate (runtime.EncodeGate).
+Grouping chunks makes each encode more efficient (6,592-row 154x518 chunks
+fill the GPU poorly one at a time) but delays the first chunk of a group, and
+a large group at the end of a rank's plan leaves many alignments to run after
+the last encode.  ``simulate`` predicts the sequence time of a set of plans
+from measured per-job costs; ``plan_ring`` searches group sizes and the DPT
+placement rank by rank (coordinate descent) for the smallest predicted time.
+Plans change only the order of work, never the results (tests/test_dist_pipeline.py).
+"""
+from __future__ import annotations
+
+import bisect
+import json
+import os
+from dataclasses import asdict, dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+Job = Tuple[str, Tuple[int, ...]]
+
+
+@dataclass
+class RingCosts:
+    """Measured costs (ms).  ``core[(frames, g)]`` / ``dense[(frames, g)]``:
+    one job over g chunks of ``frames`` frames; ``t_align``: one alignment
+    beside a gated encode, ``t_align_alone``: with the rank's encodes done;
+    ``t_pause``: encode time one alignment costs its rank (the gate's pause);
+    ``t_align_ungated`` / ``t_pause_ungated``: the same without the gate (the
+    alignment shares the CUs with the encode: slower, but it costs the encode
+    less); ``hop``: one baton send/recv between ranks; ``gather``: the end-of-sequence
+    all-gather + depth scaling."""
+    core: Dict[Tuple[int, int], float]
+    dense: Dict[Tuple[int, int], float]
+    t_align: float
+    t_align_alone: float
+    t_pause: float
+    t_align_ungated: float = 7.7
+    t_pause_ungated: float = 1.6
+    hop: float = 0.25
+    gather: float = 0.5
+    source: str = ""
+
+    def job_ms(self, kind: str, frames: int, g: int) -> float:
+        if kind == "enc":
+            return self.job_ms("core", frames, g) + self.job_ms("dense", frames, g)
+        tab = self.core if kind == "core" else self.dense
+        if (frames, g) in tab:
+            return tab[(frames, g)]
+        # nearest measured entry, scaled by the work ratio (frames x group size)
+        fr, gg = min(tab, key=lambda k: (abs(k[0] - frames), abs(k[1] - g)))
+        return tab[(fr, gg)] * (frames * g) / (fr * gg)
+
+    def to_json(self) -> dict:
+        d = asdict(self)
+        d["core"] = {f"{k[0]}x{k[1]}": v for k, v in self.core.items()}
+        d["dense"] = {f"{k[0]}x{k[1]}": v for k, v in self.dense.items()}
+        return d
+
+    @staticmethod
+    def from_json(d: dict) -> "RingCosts":
+        d = dict(d)
+        for key in ("core", "dense"):
+            d[key] = {tuple(int(x) for x in k.split("x")): float(v) for k, v in d[key].items()}
+        return RingCosts(**d)
+
+
+# Default costs: 16-frame 154x518 chunks (BASELINE configs[3] / [4]) on one MI355X,
+# measured by bench.py --config 3 (`ring_model.costs`, profiles/r9); only the RELATIVE
+# costs steer the plan.  Other shapes scale by frames x group size (job_ms).
+DEFAULT_COSTS = RingCosts(
+    core={(16, 1): 29.0, (16, 2): 51.0, (16, 3): 72.0, (8, 1): 17.0},
+    dense={(16, 1): 6.5, (16, 2): 11.5, (16, 3): 16.5, (8, 1): 3.6},
+    t_align=3.45, t_align_alone=2.62, t_pause=3.9, t_align_ungated=7.7, t_pause_ungated=1.6, hop=0.25, gather=0.5,
+    source="round-4 estimates (profiles/r8/bench/final_c3.json, profiles/r7k/c3_kernels.md)")
+
+
+def load_costs() -> RingCosts:
+    """VGGT_RING_COSTS=<json file> (a bench line's ``ring_model.costs``) or the defaults."""
+    p = os.environ.get("VGGT_RING_COSTS")
+    if p:
+        with open(p) as fh:
+            d = json.load(fh)
+        return RingCosts.from_json(d.get("ring_model", {}).get("costs", d))
+    return DEFAULT_COSTS
+
+
+# ------------------------------------------------------------------ plans
+def compositions(n: int, cap: int) -> List[Tuple[int, ...]]:
+    """All ordered ways to write n as a sum of parts in 1..cap."""
+    if n == 0:
+        return [()]
+    out = []
+    for first in range(1, min(cap, n) + 1):
+        out.extend((first,) + rest for rest in compositions(n - first, cap))
+    return out
+
+
+def candidate_sizes(n: int, cap: int, full_upto: int = 8) -> List[Tuple[int, ...]]:
+    """Group-size sequences tried for a run of n chunks: every composition
+    for short runs (a W >= 4 rank owns <= 11 of 43 chunks); for long runs
+    (W = 1, 2) a head of up to 3 chunks in any composition, a uniform middle
+    of groups of g, and a tail of up to 3 chunks in any composition."""
+    if n <= full_upto:
+        return compositions(n, cap)
+    out = set()
+    ends = [c for k in range(0, 4) for c in compositions(k, cap)]
+    for head in ends:
+        for tail in ends:
+            mid = n - sum(head) - sum(tail)
+            if mid < 0:
+                continue
+            for g in range(1, cap + 1):
+                body = (g,) * (mid // g) + ((mid % g,) if mid % g else ())
+                out.add(tuple(head) + body + tuple(tail))
+    return sorted(out)
+
+
+def runs_of(own: Sequence[int], lengths: Sequence[int]) -> List[List[int]]:
+    """Maximal runs of consecutive own chunks with equal length (only those can share an encode)."""
+    out: List[List[int]] = []
+    for i in own:
+        if out and lengths[out[-1][-1]] == lengths[i]:
+            out[-1].append(i)
+        else:
+            out.append([i])
+    return out
+
+
+def make_jobs(groups: Sequence[Sequence[int]], policy: str) -> List[Job]:
+    """Job list of one rank.  policy: "with" (DPT inside each encode), "lag"
+    (each group's DPT after the NEXT group's core), "end" (every core first)."""
+    gs = [tuple(g) for g in groups]
+    if policy == "with":
+        return [("enc", g) for g in gs]
+    if policy == "end":
+        return [("core", g) for g in gs] + [("dense", g) for g in gs]
+    if policy == "lag":
+        jobs: List[Job] = []
+        for k, g in enumerate(gs):
+            jobs.append(("core", g))
+            if k > 0:
+                jobs.append(("dense", gs[k - 1]))
+        if gs:
+            jobs.append(("dense", gs[-1]))
+        return jobs
+    raise ValueError(policy)
+
+
+def split_groups(own: Sequence[int], lengths: Sequence[int], sizes: Sequence[int]) -> List[List[int]]:
+    """Cut the rank's longest equal-length run by ``sizes``; other runs (a
+    tail chunk of another length) become groups of their own."""
+    runs = runs_of(own, lengths)
+    main = max(range(len(runs)), key=lambda k: len(runs[k])) if runs else -1
+    out: List[List[int]] = []
+    for k, run in enumerate(runs):
+        if k != main:
+            out.append(list(run))
+            continue
+        o = 0
+        for s in sizes:
+            out.append(list(run[o:o + s]))
+            o += s
+    return out
+
+
+@dataclass
+class RankPlan:
+    jobs: List[Job]
+    sizes: Tuple[int, ...] = ()
+    policy: str = "with"
+    gated: bool = True
+
+
+@dataclass
+class Prediction:
+    total_ms: float
+    align_start: List[float] = field(default_factory=list)
+    align_end: List[float] = field(default_factory=list)
+    rank_finish: List[float] = field(default_factory=list)
+
+
+def _timeline(jobs: Sequence[Job], lengths, costs: RingCosts, pauses: Sequence[float],
+              t_pause: float) -> List[float]:
+    """End time of every job on one encode stream (jobs back to back from 0);
+    each alignment starting at p while a job runs pauses that job t_pause."""
+    t = 0.0
+    ends = []
+    ps = sorted(pauses)
+    for kind, g in jobs:
+        dur = costs.job_ms(kind, lengths[g[0]], len(g))
+        start = t
+        end = start + dur
+        lo = bisect.bisect_left(ps, start)
+        while True:
+            k = bisect.bisect_left(ps, end) - lo
+            new = start + dur + k * t_pause
+            if new == end:
+                break
+            end = new
+        ends.append(end)
+        t = end
+    return ends
+
+
+def simulate(lengths: Sequence[int], W: int, plans: Sequence[RankPlan], costs: RingCosts) -> Prediction:
+    """Predicted sequence time of the ring (chunk i on rank i mod W)."""
+    n = len(lengths)
+    core_job: Dict[int, Tuple[int, int]] = {}
+    for r, pl in enumerate(plans):
+        for j, (kind, g) in enumerate(pl.jobs):
+            if kind in ("enc", "core"):
+                for i in g:
+                    core_job[i] = (r, j)
+    pauses: List[List[float]] = [[] for _ in range(W)]
+    a_s: List[float] = []
+    a_e: List[float] = []
+    tp = [costs.t_pause if pl.gated else costs.t_pause_ungated for pl in plans]
+    for i in range(n):
+        r, j = core_job[i]
+        tl = _timeline(plans[r].jobs, lengths, costs, pauses[r], tp[r])
+        s = tl[j]
+        if i > 0:
+            s = max(s, a_e[-1] + (costs.hop if W > 1 else 0.0))
+        busy = s < tl[-1]  # the rank still has encode work queued at s
+        if busy:
+            pauses[r].append(s)
+        a_s.append(s)
+        a_e.append(s + ((costs.t_align if plans[r].gated else costs.t_align_ungated) if busy
+                        else costs.t_align_alone))
+    fin = [(_timeline(pl.jobs, lengths, costs, pauses[r], tp[r]) or [0.0])[-1] for r, pl in enumerate(plans)]
+    total = max(max(fin), a_e[-1] if a_e else 0.0) + costs.gather
+    return Prediction(total, a_s, a_e, fin)
+
+
+_POLICIES = ("with", "lag", "end")
+
+
+def plan_ring(lengths: Sequence[int], W: int, costs: Optional[RingCosts] = None, cap: int = 3,
+              policies: Sequence[str] = _POLICIES, gates: Sequence[bool] = (True, False),
+              sweeps: int = 3) -> Tuple[List[RankPlan], Prediction]:
+    """Per-rank plans minimising the predicted sequence time: each rank's
+    longest equal-length run is cut into groups of <= cap chunks (every
+    composition tried) under each DPT placement policy, gated or not, rank by rank, a few
+    coordinate-descent sweeps from the best uniform choice.  Deterministic, so
+    every rank computes the same plans."""
+    costs = costs or load_costs()
+    n = len(lengths)
+    owns = [list(range(r, n, W)) for r in range(W)]
+    options: List[List[Tuple[Tuple[int, ...], str, bool]]] = []
+    for r in range(W):
+        runs = runs_of(owns[r], lengths)
+        m = max((len(x) for x in runs), default=0)
+        options.append([(c, p, gt) for c in candidate_sizes(m, cap) for p in policies for gt in gates])
+
+    def build(choice):
+        return [RankPlan(make_jobs(split_groups(owns[r], lengths, c), p), c, p, gt)
+                for r, (c, p, gt) in enumerate(choice)]
+
+    def score(choice):
+        pr = simulate(lengths, W, build(choice), costs)
+        return (round(pr.total_ms, 6), round(sum(pr.rank_finish), 6)), pr
+
+    # start: the best choice applied to every rank alike (by pattern of the largest rank)
+    best = None
+    for c, p, gt in options[0]:
+        choice = []
+        for r in range(W):
+            m = sum(c)
+            mine = max((len(x) for x in runs_of(owns[r], lengths)), default=0)
+            cc = c if mine == m else _fit(c, mine, cap)
+            choice.append((cc, p, gt))
+        sc, pr = score(choice)
+        if best is None or sc < best[0]:
+            best = (sc, choice, pr)
+    sc, choice, pr = best
+    for _ in range(sweeps):
+        changed = False
+        for r in range(W):
+            for opt in options[r]:
+                if opt == choice[r]:
+                    continue
+                trial = list(choice)
+                trial[r] = opt
+                s2, p2 = score(trial)
+                if s2 < sc:
+                    sc, choice, pr, changed = s2, trial, p2, True
+        if not changed:
+            break
+    return build(choice), pr
+
+
+def _fit(c: Tuple[int, ...], m: int, cap: int) -> Tuple[int, ...]:
+    """Adapt a composition to a run of m chunks: trim from the front or extend with 1s at the front."""
+    c = list(c)
+    while sum(c) > m:
+        c[0] -= 1
+        if c[0] == 0:
+            c.pop(0)
+    while sum(c) < m:
+        c.insert(0, 1)
+    return tuple(c)
+
+
+def legacy_plans(lengths: Sequence[int], W: int, cap: int = 3) -> List[RankPlan]:
+    """Round-4 schedule for comparison: each rank's own consecutive equal-length
+    chunks greedily in groups of ``cap``, DPT inside each encode."""
+    n = len(lengths)
+    plans = []
+    for r in range(W):
+        groups: List[List[int]] = []
+        for i in range(r, n, W):
+            if groups and len(groups[-1]) < cap and lengths[groups[-1][-1]] == lengths[i]:
+                groups[-1].append(i)
+            else:
+                groups.append([i])
+        plans.append(RankPlan(make_jobs(groups, "with"), tuple(len(g) for g in groups), "with"))
+    return plans
+
+
+def enqueue_order(plan: RankPlan, own: Sequence[int]) -> List[Tuple[str, Tuple[int, ...]]]:
+    """The host-side order in which the ring issues this rank's work: its jobs
+    in plan order, and alignment i right after the job FOLLOWING the one that
+    produced chunk i's core (one job of look-ahead keeps the encode stream
+    fed while the host waits on a host-blocking baton; over RCCL nothing
+    blocks).  Returns ("job", chunks) / ("align", (i,)) entries."""
+    jobs = plan.jobs
+    core_at = {}
+    for j, (kind, g) in enumerate(jobs):
+        if kind in ("enc", "core"):
+            for i in g:
+                core_at[i] = j
+    out: List[Tuple[str, Tuple[int, ...]]] = []
+    issued = -1
+    for i in own:
+        need = min(core_at[i] + 1, len(jobs) - 1)
+        while issued < need:
+            issued += 1
+            out.append(("job", issued))
+        out.append(("align", (i,)))
+    while issued < len(jobs) - 1:
+        issued += 1
+        out.append(("job", issued))
+    return out
+
+
+def predict_scaling(lengths: Sequence[int], costs: RingCosts, worlds=(1, 2, 4, 8)) -> dict:
+    """Predicted sequence time at each W (the planner's plans) and, for
+    comparison, the round-4 schedule's."""
+    out = {}
+    for W in worlds:
+        plans, pr = plan_ring(lengths, W, costs)
+        leg = simulate(lengths, W, legacy_plans(lengths, W), costs)
+        out[str(W)] = {"T_ms": round(pr.total_ms, 1), "T_ms_round4_schedule": round(leg.total_ms, 1),
+                       "plans": [{"groups": [list(g) for k, g in pl.jobs if k in ("enc", "core")],
+                                  "policy": pl.policy, "gated": pl.gated} for pl in plans[:min(W, 3)]]}
+    return out

@@ -112,7 +112,13 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
                     f"does (requires_grad=False)")
 
     @torch.no_grad()
-    def encode_chunk(self, images: torch.Tensor) -> dict:
+    def encode_chunk(self, images: torch.Tensor, dense: bool = True) -> dict:
+        """Everything of the chunk's forward that does not depend on other
+        chunks.  dense=False leaves out the DPT heads (``encode_dense`` runs
+        them later): the alignment recurrence needs only the aggregator tokens,
+        the camera head and the alignment head's prefix, so the multi-GPU
+        pipeline can align a chunk before its depth maps exist
+        (dist/schedule.py)."""
         B, S, C, H, W = images.shape
         toks, patch_start_idx = self.aggregator(images, keep_layers=self.intermediate_layer_indices)
         enc = {"images": images, "tokens": toks, "patch_start_idx": patch_start_idx}
@@ -120,12 +126,6 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
         if self.camera_head is not None:
             yield_point()
             enc["cam_pose_enc"] = self.camera_head(toks)[-1]
-        if self.depth_head is not None:
-            yield_point()
-            enc["depth"], enc["depth_conf"] = self.depth_head(toks, images=images, patch_start_idx=patch_start_idx)
-        if self.point_head is not None:
-            yield_point()
-            enc["points"], enc["points_conf"] = self.point_head(toks, images=images, patch_start_idx=patch_start_idx)
         if _ALIGN_PREFIX and not self.alignment_head.training and images.is_cuda:
             yield_point()
             # the alignment head's context-free prefix, as (B, S*(P+1), C) rows so a
@@ -133,7 +133,62 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
             P1 = toks[-1].shape[2] + 1
             x = self.alignment_head.prepare_infer(toks[-1], (H, W))
             enc["ah_prep"] = x[:B * S * P1].view(B, S * P1, x.shape[1])
+        if dense:
+            self.encode_dense(enc)
         return enc
+
+    @torch.no_grad()
+    def encode_dense(self, enc: dict) -> dict:
+        """The DPT depth / point heads of an ``encode_chunk(..., dense=False)``
+        result (featureAligned_vggt.py:165-216 before the Sim(3) scaling), in place."""
+        toks, images, psi = enc["tokens"], enc["images"], enc["patch_start_idx"]
+        if self.depth_head is not None:
+            yield_point()
+            enc["depth"], enc["depth_conf"] = self.depth_head(toks, images=images, patch_start_idx=psi)
+        if self.point_head is not None:
+            yield_point()
+            enc["points"], enc["points_conf"] = self.point_head(toks, images=images, patch_start_idx=psi)
+        return enc
+
+    @torch.no_grad()
+    def scale_dense(self, enc: dict, chunk_sim3_enc: torch.Tensor) -> dict:
+        """Depth outputs of a chunk whose DPT head ran after its alignment:
+        depth *= chunk scale (featureAligned_vggt.py:171, in place), as
+        align_chunk does when the depth is already there."""
+        if "depth" not in enc:
+            return {}
+        B = enc["depth"].shape[0]
+        return {"depth": N.scale_(enc["depth"], chunk_sim3_enc[..., -1].reshape(B)), "depth_conf": enc["depth_conf"]}
+
+    def prepare_align(self, enc: dict, num_overlap: int, context: dict = None, gt_poses: torch.Tensor = None) -> None:
+        """Everything align_chunk may do that synchronises the device, done
+        ahead of it: with VGGT_ALIGN_GRAPH=1 the first chunk of each shape
+        captures its HIP graph (torch.cuda.graph synchronises).  The pipeline
+        calls this before it gates its encode stream (runtime.EncodeGate)."""
+        if not _ALIGN_GRAPH or self.alignment_head.trainable():
+            return
+        core_in = self._core_inputs(enc, num_overlap, context, gt_poses)
+        if core_in is not None:
+            self._align_graph_get(core_in)
+
+    def _core_inputs(self, enc, num_overlap, context, gt_poses):
+        """The inputs of _align_core for this chunk (None: the prefix did not run in the encode)."""
+        prep = enc.get("ah_prep")
+        if prep is None:
+            return None
+        images, toks = enc["images"], enc["tokens"]
+        B, S, C, H, W = images.shape
+        ctx_overlap = ctx_memory = None
+        if context is not None:
+            ctx_overlap = context["overlap_tokens"]
+            if self.enable_memory:
+                ctx_memory = context["memory_tokens"][-1]
+        overlap = num_overlap if S > num_overlap else S - 1
+        mode = "torch" if images.device.type != "cuda" else _POSE_MODE
+        ctx_pe = context["pose_enc"][-1] if context is not None else None
+        use_pose = self.camera_head is not None and mode == "hip" and (context is None or gt_poses is None)
+        return (prep, (B, S, toks[-1].shape[2]), (H, W), overlap, ctx_overlap, ctx_memory,
+                enc["cam_pose_enc"] if use_pose else None, ctx_pe if use_pose else None, self.point_head is not None)
 
     def align_chunk(self, enc: dict, num_overlap: int, context: dict = None, gt_poses: torch.Tensor = None) -> dict:
         train = self.alignment_head.trainable()
@@ -153,14 +208,10 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
         overlap = num_overlap if S > num_overlap else S - 1
         dev = images.device
         mode = "torch" if train or dev.type != "cuda" else _POSE_MODE
-        prep = enc.get("ah_prep") if not train else None
+        core_in = self._core_inputs(enc, num_overlap, context, gt_poses) if not train else None
         pre = None  # (aligned_pose_enc, point_transform) when composed with the head
-        if prep is not None:
-            ctx_pe = context["pose_enc"][-1] if context is not None else None
-            use_pose = self.camera_head is not None and mode == "hip" and (context is None or gt_poses is None)
-            core_in = (prep, (B, S, toks[-1].shape[2]), (H, W), overlap, ctx_overlap, ctx_memory,
-                       enc["cam_pose_enc"] if use_pose else None, ctx_pe if use_pose else None,
-                       self.point_head is not None)
+        if core_in is not None:
+            use_pose = core_in[6] is not None
             if _ALIGN_GRAPH:
                 outs = self._align_graph(core_in)
             else:
@@ -206,7 +257,7 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
                     context.setdefault("memory_tokens", []).append(memory_tokens)
                     predictions["memory_tokens"] = context["memory_tokens"]
 
-        if self.depth_head is not None:
+        if self.depth_head is not None and "depth" in enc:  # not yet there: scale_dense, after encode_dense
             if train:  # d chunk_scale = sum(d depth * depth_raw)
                 depth = AG.ScaleFn.apply(enc["depth"], chunk_scale.reshape(B))
             else:
@@ -221,7 +272,7 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
                 context.setdefault("depth_conf", []).append(depth_conf)
                 predictions["depth_conf"] = context["depth_conf"]
 
-        if self.point_head is not None:
+        if self.point_head is not None and "points" in enc:
             pts3d, pts3d_conf = enc["points"], enc["points_conf"]
             if self.camera_head is not None:
                 pt = point_transform
@@ -251,6 +302,10 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
     def _align_graph(self, core_in):
         """Replay the recurrent part of align_chunk from a HIP graph captured
         for this shape (and these parameter values)."""
+        return self._align_graph_get(core_in)(core_in)
+
+    def _align_graph_get(self, core_in) -> "_AlignGraph":
+        """The captured graph for this shape (captured on first use)."""
         prep, bsp, hw, overlap, ctx_ov, ctx_mem, cam, ctx_pe, want_pt = core_in
         head = self.alignment_head
         sig = tuple((p.data_ptr(), p._version) for p in head.parameters())
@@ -260,7 +315,7 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
         g = graphs.get(key)
         if g is None or g.sig != sig:
             g = graphs[key] = _AlignGraph(head, core_in, sig)
-        return g(core_in)
+        return g
 
     def _compose_torch(self, enc, chunk_sim3_enc, frame_se3_enc, context, gt_poses, overlap, images, adev):
         """featureAligned_vggt.py:96-143 (+ the point transform of :187-196) as torch

@@ -224,7 +224,29 @@ def _hip():
         _HIP.hipStreamWaitValue32.restype = ctypes.c_int
         _HIP.hipStreamWriteValue32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint]
         _HIP.hipStreamWriteValue32.restype = ctypes.c_int
+        _HIP.hipStreamGetPriority.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+        _HIP.hipStreamGetPriority.restype = ctypes.c_int
+        _HIP.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+        _HIP.hipStreamDestroy.restype = ctypes.c_int
     return _HIP
+
+
+def stream_priority(stream) -> int:
+    """The HIP priority of a torch stream (lower = higher priority; the null stream's is 0)."""
+    import ctypes
+    p = ctypes.c_int(0)
+    rc = _hip().hipStreamGetPriority(ctypes.c_void_p(stream.cuda_stream), ctypes.byref(p))
+    if rc != 0:
+        raise RuntimeError(f"hipStreamGetPriority failed ({rc})")
+    return p.value
+
+
+def destroy_stream(stream) -> None:
+    """hipStreamDestroy a stream this package created (dedicated_stream / cu_masked_stream)."""
+    import ctypes
+    rc = _hip().hipStreamDestroy(ctypes.c_void_p(stream.cuda_stream))
+    if rc != 0:
+        raise RuntimeError(f"hipStreamDestroy failed ({rc})")
 
 
 class EncodeGate:
@@ -235,9 +257,22 @@ class EncodeGate:
     and 0 when it is done (hipStreamWriteValue32); the encode stream, at its
     yield points (`yield_point`, between transformer blocks and heads), waits
     for 0 (hipStreamWaitValue32).  An alignment therefore shares the GPU with
-    at most one yield interval of encode work and then runs alone.  No cycle:
-    the word goes to 1 only after the chunk's own encode has finished, and the
-    alignment never waits on the encode stream after that."""
+    at most one yield interval of encode work and then runs alone.
+
+    Why it cannot deadlock (the rules the pipeline keeps):
+      * the word goes to 1 only after the chunk's own encode has finished, and
+        the alignment stream never waits on the encode stream after that;
+      * no device-wide wait between begin and end: a hipDeviceSynchronize (a
+        HIP graph capture's, an allocator's hipFree on an out-of-memory retry)
+        issued by the host while the gate is held would wait for the paused
+        encode, which waits for the end() the host has not enqueued yet.  The
+        ring therefore runs ``prepare_align`` (graph capture) before begin();
+      * the alignment stream has a strictly higher priority than the encode
+        stream (checked before the gate is used, else the ring runs ungated):
+        HIP maps priorities to separate hardware-queue pools, so with
+        GPU_MAX_HW_QUEUES = 4 and more normal-priority streams than queues the
+        encode's spinning wait can share a queue with other normal streams but
+        never sits ahead of the alignment's begin/end writes in one queue."""
 
     def __init__(self, device):
         import ctypes

@@ -17,6 +17,14 @@ import glob
 import json
 import os
 import statistics
+import sys
+
+
+def _stamp():
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "large-scale-vit-slam_amd"))
+    from aligned_vggt.provenance import stamp
+    return stamp()
 
 
 def _rows(d):
@@ -62,7 +70,8 @@ def main():
     traffic = 2.0 * fetch_kb * 1024 + write_kb * 1024
     res = {"kernel": a.kernel, "grid": a.grid, "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
            "launches": [nf, nw], "hbm_bytes_per_launch": traffic,
-           "correction": "FETCH_SIZE x2 (gfx950 16-B/lane streaming reads), WRITE_SIZE x1"}
+           "correction": "FETCH_SIZE x2 (gfx950 16-B/lane streaming reads), WRITE_SIZE x1",
+           **_stamp()}
     print(json.dumps(res))
     if a.out:
         with open(a.out, "w") as fh:

@@ -21,6 +21,7 @@ import csv
 import glob
 import json
 import os
+import sys
 
 
 def rows(d):
@@ -90,6 +91,10 @@ def main():
     if busy_pass:
         g = tot[f"GRBM_GUI_ACTIVE@{busy_pass}"] / 8
         out["kernel_cycles_per_xcd"] = g
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "large-scale-vit-slam_amd"))
+    from aligned_vggt.provenance import stamp
+    out.update(stamp())
     print(json.dumps(out, indent=1))
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)

@@ -57,11 +57,14 @@ def _model(cuda, monkeypatch, depth=4):
     return m.to(cuda).eval()
 
 
-@pytest.mark.parametrize("group,reserve", [(1, 0), (3, 0), (3, 16)])
-def test_overlapped_schedule_matches_sequential_loop(cuda, monkeypatch, group, reserve):
+@pytest.mark.parametrize("group,reserve,policy", [(1, 0, "with"), (3, 0, "with"), (3, 16, "with"), (2, 0, "lag"),
+                                                  (3, 0, "end")])
+def test_overlapped_schedule_matches_sequential_loop(cuda, monkeypatch, group, reserve, policy):
     """The side-stream schedule (align on its own stream, concurrent with the
-    next encode group; optionally the encodes on a CU-masked stream) is bitwise
-    equal to the sequential chunk loop."""
+    next encode job; optionally the encodes on a CU-masked stream; the DPT
+    heads with each encode, one group behind or after every core -- then the
+    depth maps are scaled after their alignment) is bitwise equal to the
+    sequential chunk loop."""
     from aligned_vggt.dist.pipeline import ChunkPipeline, apply_sequence_to_model
     from aligned_vggt.utils.data import generate_chunks
     from aligned_vggt.utils.synthetic import synthetic_images
@@ -73,6 +76,8 @@ def test_overlapped_schedule_matches_sequential_loop(cuda, monkeypatch, group, r
     P1 = 6 + (H // 14) * (W // 14)
     pipe = ChunkPipeline(m, device=cuda, gather_dense=True, encode_group=group, overlap_align=True, time_align=True)
     pipe.reserve_cus = reserve  # > 0: encodes on a stream masked off that many CUs
+    pipe.plan_policies = (policy,)
+    pipe.plan_gates = (True,)
     for _ in range(2):  # the second run reuses every per-stream buffer
         got = pipe.run(imgs, w, ov, token_dims=(P1, 1024), memory_shape=(1, 8, 512))
         torch.cuda.synchronize()
@@ -83,7 +88,53 @@ def test_overlapped_schedule_matches_sequential_loop(cuda, monkeypatch, group, r
     t = pipe.align_ms()
     n = len(generate_chunks(N_, "chunk_overlap", w, ov))
     assert len(t) == n and all(x > 0 for x in t), t
+    assert pipe.__dict__.get("_gate") is not None  # the alignment stream outranks the encode stream: gated
+    kinds = {k for _, k, _ in (e for e in pipe.enqueue_log if e[0] == "job")}
+    assert kinds == ({"enc"} if policy == "with" else {"core", "dense"}), kinds
     print("align_chunk ms under concurrent encodes:", [round(x, 3) for x in t])
+    pipe.close()
+
+
+def test_gated_ring_with_align_graph(cuda, monkeypatch):
+    """with VGGT_ALIGN_GRAPH=1 the first alignment of each shape
+    captures a HIP graph, and capture synchronises the device.  The ring does
+    that capture (prepare_align) before it closes the encode gate, so a gated
+    encode never waits for a gate the host cannot release; results equal the
+    sequential loop's eager path to fp32 round-off."""
+    from aligned_vggt.dist.pipeline import ChunkPipeline, apply_sequence_to_model
+    from aligned_vggt.models import featureAligned_vggt as FAmod
+    from aligned_vggt.utils.synthetic import synthetic_images
+    m = _model(cuda, monkeypatch)
+    N_, w, ov, H, W = 30, 8, 2, 56, 70  # a shorter tail chunk: two graph shapes
+    imgs = synthetic_images(1, N_, H, W, seed=12).to(cuda)
+    ref = apply_sequence_to_model({"images": imgs}, m, [w], [ov], "chunk_overlap", None)
+    monkeypatch.setattr(FAmod, "_ALIGN_GRAPH", True)
+    P1 = 6 + (H // 14) * (W // 14)
+    with ChunkPipeline(m, device=cuda, gather_dense=True, encode_group=2, overlap_align=True) as pipe:
+        pipe.plan_gates = (True,)
+        for _ in range(2):  # first run captures inside the ring, second replays
+            got = pipe.run(imgs, w, ov, token_dims=(P1, 1024), memory_shape=(1, 8, 512))
+            torch.cuda.synchronize()
+        assert pipe.__dict__.get("_gate") is not None
+    assert m.__dict__.get("_mi355x_align_graphs"), "no graph was captured"
+    for k in ("pose_enc", "chunk_sim3_alignment_enc", "frame_se3_alignment_enc", "depth"):
+        a, b = got[k].cpu(), ref[k].cpu()
+        e = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+        assert e < 1e-5, (k, e)
+
+
+def test_pipeline_close_releases_streams(cuda):
+    """dedicated streams, their library configuration slots
+    (vggt_set_stream_config has 16) and the gate's signal word are released by
+    close(): 20 short-workgroup pipelines in a row do not run out of slots."""
+    from aligned_vggt.dist.pipeline import ChunkPipeline
+    from aligned_vggt.runtime import stream_priority
+    for _ in range(20):
+        pipe = ChunkPipeline(None, device=cuda, short_workgroups=True, gate_encode=False)
+        s = pipe._encode_stream()
+        side = pipe._align_stream(True)
+        assert stream_priority(side) < stream_priority(s)
+        pipe.close()
 
 
 @pytest.mark.parametrize("H,W,w,ov,nm", [(56, 70, 8, 2, 8), (42, 56, 5, 1, 0)])

@@ -15,12 +15,24 @@ class ToyAlignModel:
     forward + reference context semantics), tiny CPU arithmetic with a real
     dependence on the previous chunk's overlap tokens, memory and poses."""
 
-    def encode_chunk(self, images):
+    point_head = None
+
+    def encode_chunk(self, images, dense=True):
         B, S = images.shape[:2]
         f = images.mean(dim=(2, 3, 4))  # (B, S)
         tok = f[:, :, None, None] * torch.arange(1, P1 * C + 1, dtype=torch.float32).view(1, 1, P1, C) / 100
-        return {"images": images, "tok": tok, "depth": images[:, :, :1].permute(0, 1, 3, 4, 2) * 2,
-                "depth_conf": images[:, :, 1] + 1}
+        enc = {"images": images, "tok": tok}
+        return self.encode_dense(enc) if dense else enc
+
+    def encode_dense(self, enc):
+        images = enc["images"]
+        enc["depth"] = images[:, :, :1].permute(0, 1, 3, 4, 2) * 2
+        enc["depth_conf"] = images[:, :, 1] + 1
+        return enc
+
+    def scale_dense(self, enc, sim3):
+        B = enc["depth"].shape[0]
+        return {"depth": enc["depth"] * sim3[..., -1].view(B, 1, 1, 1, 1), "depth_conf": enc["depth_conf"]}
 
     def align_chunk(self, enc, num_overlap, context=None):
         tok = enc["tok"].clone()
@@ -38,11 +50,14 @@ class ToyAlignModel:
         sim3 = tok.mean(dim=(1, 2, 3))[:, None, None].expand(B, 1, 8).clone()
         fse3 = tok[:, 1:].mean(dim=(2, 3))[..., None].expand(B, S - 1, 7).clone()
         scale = sim3[..., -1]
-        depth = enc["depth"] * scale.view(B, 1, 1, 1, 1)
+        dense = "depth" in enc  # else the pipeline scales it after encode_dense (scale_dense)
+        depth = enc["depth"] * scale.view(B, 1, 1, 1, 1) if dense else None
         pred = {"overlap_tokens": torch.cat([tok[:, :1], tok[:, -ov:]], 1).contiguous()}
         if context is None:
             pred.update(pose_enc=[pose], chunk_sim3_alignment_enc=sim3, frame_se3_alignment_enc=fse3,
-                        memory_tokens=[mem], depth=[depth], depth_conf=[enc["depth_conf"]])
+                        memory_tokens=[mem])
+            if dense:
+                pred.update(depth=[depth], depth_conf=[enc["depth_conf"]])
         else:
             context.setdefault("pose_enc", []).append(pose)
             pred["pose_enc"] = context["pose_enc"]
@@ -50,7 +65,7 @@ class ToyAlignModel:
             pred["frame_se3_alignment_enc"] = merge_results(context["frame_se3_alignment_enc"], fse3)
             context.setdefault("memory_tokens", []).append(mem)
             pred["memory_tokens"] = context["memory_tokens"]
-            for k, v in (("depth", depth), ("depth_conf", enc["depth_conf"])):
+            for k, v in ((("depth", depth), ("depth_conf", enc["depth_conf"])) if dense else ()):
                 context.setdefault(k, []).append(v)
                 pred[k] = context[k]
         return pred
