@@ -218,20 +218,12 @@ class ChunkPipeline:
 
     # ------------------------------------------------------------ lifetime
     def close(self) -> None:
-        """Release what the pipeline created on the device: the encode gate's
-        signal word, the library's per-stream configuration slots and the
-        dedicated HIP streams."""
-        from ..runtime import destroy_stream
+        """Release what the pipeline owns on the device: the encode gate's
+        signal word.  Its HIP streams are process-wide (runtime.shared_stream),
+        reused by every pipeline with the same configuration."""
         gate = self.__dict__.pop("_gate", None)
         if gate is not None:
             gate.close()
-        owned = self.__dict__.pop("_owned_streams", [])
-        if owned:
-            from .. import _native as N
-            torch.cuda.synchronize(self.device)
-            for s in owned:
-                N.set_stream_config(s.cuda_stream, 0, 0)  # frees the slot (capi.cpp)
-                destroy_stream(s)
         self.__dict__.pop("_enc_streams", None)
         self.__dict__.pop("_align_streams", None)
 
@@ -354,29 +346,13 @@ class ChunkPipeline:
         return self._gather(mine, chunks, num_overlap, B)
 
     def _encode_stream(self):
-        """The ring's encode stream (cached per configuration): a dedicated
-        non-blocking HIP stream, or one masked off `reserve_cus` CUs, registered
-        with the library (vggt_set_stream_config) so its persistent kernels size
-        their grids to the CUs it can use and, with short_workgroups, it gets no
-        persistent GEMM forms at all."""
-        from .. import _native as N
-        from ..runtime import cu_masked_stream, dedicated_stream, spread_cus
-        key = (self.reserve_cus, self.short_workgroups)
-        streams = self.__dict__.setdefault("_enc_streams", {})
-        s = streams.get(key)
-        if s is None:
-            cus = 0
-            if self.reserve_cus > 0:
-                ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
-                excl = spread_cus(ncu, self.reserve_cus)
-                s = cu_masked_stream(self.device, excl)
-                cus = ncu - len(excl)
-            else:
-                s = dedicated_stream(self.device)
-            N.set_stream_config(s.cuda_stream, cus, N.STREAM_SHORT_WORKGROUPS if self.short_workgroups else 0)
-            streams[key] = s
-            self.__dict__.setdefault("_owned_streams", []).append(s)
-        return s
+        """The ring's encode stream: a dedicated non-blocking HIP stream, or one
+        masked off `reserve_cus` CUs, registered with the library
+        (vggt_set_stream_config) so its persistent kernels size their grids to
+        the CUs it can use and, with short_workgroups, it gets no persistent
+        GEMM forms at all (runtime.shared_stream)."""
+        from ..runtime import shared_stream
+        return shared_stream(self.device, exclude_cus=self.reserve_cus, short_workgroups=self.short_workgroups)
 
     def _groups(self, chunks, own: List[int], images) -> List[List[int]]:
         """Encode groups over this rank's own chunks (runs of equal length)."""
@@ -487,11 +463,8 @@ class ChunkPipeline:
                 # a dedicated high-priority stream, also short-workgroup: beside an encode its
                 # GEMMs' tiles go to whichever CUs free up first instead of one persistent
                 # workgroup per CU that starts only when its CU does
-                from .. import _native as N
-                from ..runtime import dedicated_stream
-                side = dedicated_stream(self.device, priority=hi)
-                N.set_stream_config(side.cuda_stream, 0, N.STREAM_SHORT_WORKGROUPS)
-                self.__dict__.setdefault("_owned_streams", []).append(side)
+                from ..runtime import shared_stream
+                side = shared_stream(self.device, priority=hi, short_workgroups=True)
             else:
                 side = torch.cuda.Stream(self.device, priority=hi)
             streams[align_short] = side

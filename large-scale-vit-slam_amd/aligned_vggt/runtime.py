@@ -226,8 +226,6 @@ def _hip():
         _HIP.hipStreamWriteValue32.restype = ctypes.c_int
         _HIP.hipStreamGetPriority.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
         _HIP.hipStreamGetPriority.restype = ctypes.c_int
-        _HIP.hipStreamDestroy.argtypes = [ctypes.c_void_p]
-        _HIP.hipStreamDestroy.restype = ctypes.c_int
     return _HIP
 
 
@@ -239,14 +237,6 @@ def stream_priority(stream) -> int:
     if rc != 0:
         raise RuntimeError(f"hipStreamGetPriority failed ({rc})")
     return p.value
-
-
-def destroy_stream(stream) -> None:
-    """hipStreamDestroy a stream this package created (dedicated_stream / cu_masked_stream)."""
-    import ctypes
-    rc = _hip().hipStreamDestroy(ctypes.c_void_p(stream.cuda_stream))
-    if rc != 0:
-        raise RuntimeError(f"hipStreamDestroy failed ({rc})")
 
 
 class EncodeGate:
@@ -378,3 +368,36 @@ def cu_masked_stream(device, exclude) -> "torch.cuda.ExternalStream":
     if rc != 0:
         raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
     return torch.cuda.ExternalStream(s.value, device=device)
+
+
+_SHARED_STREAMS: Dict[tuple, "torch.cuda.ExternalStream"] = {}
+
+
+def shared_stream(device, exclude_cus: int = 0, priority: int = 0, short_workgroups: bool = False):
+    """The pipeline's dedicated streams, one per (device, configuration) for the
+    life of the process: a non-blocking stream (dedicated_stream) or one masked
+    off ``exclude_cus`` CUs spread over the XCDs (cu_masked_stream), registered
+    once with the library (vggt_set_stream_config: the CUs its persistent grids
+    may size to, short workgroups).  Shared rather than created per pipeline:
+    the library has 16 configuration slots, and a stream cannot be destroyed
+    while the caching allocator may still record events on it for blocks it
+    handed out there (torch keeps no count of them)."""
+    device = torch.device(device)
+    if device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    key = (device, exclude_cus, priority, short_workgroups)
+    s = _SHARED_STREAMS.get(key)
+    if s is None:
+        from . import _native as N
+        cus = 0
+        if exclude_cus > 0:
+            ncu = torch.cuda.get_device_properties(device).multi_processor_count
+            excl = spread_cus(ncu, exclude_cus)
+            s = cu_masked_stream(device, excl)
+            cus = ncu - len(excl)
+        else:
+            s = dedicated_stream(device, priority=priority)
+        if cus or short_workgroups:
+            N.set_stream_config(s.cuda_stream, cus, N.STREAM_SHORT_WORKGROUPS if short_workgroups else 0)
+        _SHARED_STREAMS[key] = s
+    return s

@@ -74,12 +74,22 @@ def gelu(x: Tensor, bf16: bool) -> Tensor:
     return _r(F.gelu(x), bf16)
 
 
-def sdpa(q: Tensor, k: Tensor, v: Tensor, bf16: bool) -> Tensor:
-    """softmax(q k^T / sqrt(d)) v over (..., N, D); fp32 softmax."""
+def sdpa(q: Tensor, k: Tensor, v: Tensor, bf16: bool, max_score_bytes: int = 1 << 31) -> Tensor:
+    """softmax(q k^T / sqrt(d)) v over (..., N, D); fp32 softmax.  Rows are
+    independent, so a score matrix larger than max_score_bytes (the global
+    attention of a 16 x 518^2 chunk: 16 x 21,984^2 fp32 = 31 GB) is formed in
+    blocks of query rows."""
     q, k, v = _r(q, bf16), _r(k, bf16), _r(v, bf16)
-    s = (q @ k.transpose(-1, -2)) * (q.shape[-1] ** -0.5)
-    p = torch.softmax(s, dim=-1)
-    return _r(p @ v, bf16)
+    nq, nk = q.shape[-2], k.shape[-2]
+    per_row = 4 * nk * max(1, q.numel() // (nq * q.shape[-1]))
+    step = max(1, min(nq, max_score_bytes // max(1, per_row)))
+    outs = []
+    for r0 in range(0, nq, step):
+        s = (q[..., r0:r0 + step, :] @ k.transpose(-1, -2)) * (q.shape[-1] ** -0.5)
+        p = torch.softmax(s, dim=-1)
+        outs.append(p @ v)
+        del s, p
+    return _r(outs[0] if len(outs) == 1 else torch.cat(outs, dim=-2), bf16)
 
 
 # ----------------------------------------------------------------------------

@@ -123,52 +123,20 @@ def test_gated_ring_with_align_graph(cuda, monkeypatch):
         assert e < 1e-5, (k, e)
 
 
-def test_pipeline_close_releases_streams(cuda):
-    """dedicated streams, their library configuration slots
-    (vggt_set_stream_config has 16) and the gate's signal word are released by
-    close(): 20 short-workgroup pipelines in a row do not run out of slots."""
+def test_pipeline_streams_are_shared(cuda):
+    """pipelines must not leak HIP streams or the library's 16
+    stream-configuration slots: their dedicated streams are process-wide per
+    configuration (runtime.shared_stream), so 20 short-workgroup pipelines in
+    a row use one encode and one alignment stream; the alignment stream
+    outranks the encode stream (the gate's condition)."""
     from aligned_vggt.dist.pipeline import ChunkPipeline
     from aligned_vggt.runtime import stream_priority
+    seen = set()
     for _ in range(20):
         pipe = ChunkPipeline(None, device=cuda, short_workgroups=True, gate_encode=False)
         s = pipe._encode_stream()
         side = pipe._align_stream(True)
         assert stream_priority(side) < stream_priority(s)
+        seen.add((s.cuda_stream, side.cuda_stream))
         pipe.close()
-
-
-@pytest.mark.parametrize("H,W,w,ov,nm", [(56, 70, 8, 2, 8), (42, 56, 5, 1, 0)])
-def test_graphed_prefix_align_matches_eager(cuda, monkeypatch, H, W, w, ov, nm):
-    """align_chunk's inference paths -- the alignment head's context-free prefix
-    (project_in, token_norm, frame block 0) run in encode_chunk (default), and with
-    it the recurrent rest replayed from one HIP graph per shape (VGGT_ALIGN_GRAPH=1)
-    -- against the eager whole-head path (VGGT_ALIGN_PREFIX=0) over a sequence with
-    a shorter tail chunk (two graph shapes) and repeated graph replays."""
-    from aligned_vggt.dist.pipeline import apply_sequence_to_model
-    from aligned_vggt.models import featureAligned_vggt as FAmod
-    from aligned_vggt.utils.synthetic import synthetic_images
-    m = _model(cuda, monkeypatch)
-    if nm == 0:
-        from aligned_vggt.heads.alignment_head import AlignmentHead
-        from aligned_vggt.utils.synthetic import condition_pose_outputs_, synthetic_init_
-        m.alignment_head = AlignmentHead(in_dim=2048, num_memory_tokens=0).to(cuda).eval()
-        m.enable_memory = False
-        synthetic_init_(m.alignment_head, seed=5)
-        condition_pose_outputs_(m)
-    N_ = 3 * w
-    imgs = synthetic_images(1, N_, H, W, seed=9).to(cuda)
-    outs = {}
-    for tag, flags in (("eager", (False, False)), ("prefix", (False, True)), ("graph", (True, True))):
-        monkeypatch.setattr(FAmod, "_ALIGN_GRAPH", flags[0])
-        monkeypatch.setattr(FAmod, "_ALIGN_PREFIX", flags[1])
-        for _ in range(2 if tag == "graph" else 1):  # the second pass replays the captured graphs
-            outs[tag] = apply_sequence_to_model({"images": imgs}, m, [w], [ov], "chunk_overlap", None)
-        torch.cuda.synchronize()
-    assert m.__dict__.get("_mi355x_align_graphs"), "no graph was captured"
-    for tag in ("prefix", "graph"):
-        for k in ("pose_enc", "chunk_sim3_alignment_enc", "frame_se3_alignment_enc", "depth"):
-            a, b = outs[tag][k].cpu(), outs["eager"][k].cpu()
-            assert a.shape == b.shape, (tag, k)
-            e = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
-            print(f"{tag} vs eager {k}: rel-L2 {e:.2e}")
-            assert e < 1e-5, (tag, k, e)
+    assert len(seen) == 1, seen
