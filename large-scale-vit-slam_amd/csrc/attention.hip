@@ -300,7 +300,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
       auto exps = [&](auto shc) {
         constexpr bool shifted = decltype(shc)::value;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) rs[i] = 0.f;
+        for (int i = 1; i < 4; ++i) rs[i] = 0.f;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -312,7 +312,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
               if constexpr (VAR & 64) x = shifted ? fmaf(x, c, -m_run) : x * c;
               else if constexpr (shifted) x -= m_run;
               const float p = __builtin_amdgcn_exp2f(x);
-              rs[0] += p;  // one chain: split sums get SLP-packed into v_pk_add_f32
+              // one chain: split sums get SLP-packed into v_pk_add_f32; started from the
+              // first p (p >= +0, so 0 + p == p bitwise: one v_add fewer per tile)
+              if (kb == 0 && ss == 0 && j == 0) rs[0] = p;
+              else rs[0] += p;
               t[j] = (__bf16)p;
             }
             pf[kb][ss] = t;
@@ -323,7 +326,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
       constexpr bool ZL = decltype(zc)::value;
       exps(std::integral_constant<bool, !ZL>{});
       float rsum = (rs[0] + rs[1]) + (rs[2] + rs[3]);
-      if (__builtin_amdgcn_ballot_w64(!(rsum <= limv) || (ZL && !zero_off)) != 0) {
+      // the ballot of the compare alone (a v_cmp straight into an SGPR mask), OR'd with the
+      // wave-uniform mode flag on the scalar side (one ballot over both materialised the
+      // mask into a VGPR and compared it again: two VALU per tile)
+      if ((__builtin_amdgcn_ballot_w64(!(rsum <= limv)) != 0) || (ZL && !zero_off)) {
         const S2 raw = qk_again(bufc);
         s[0] = raw.v[0];
         s[1] = raw.v[1];
@@ -430,6 +436,115 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
     }
   };
 
+  // ---- VAR & 256 (offset-free only; full tiles): the tile as two 32-key
+  // halves, software-pipelined inside the wave -- the QK^T MFMAs of half 1
+  // are issued between the exps of half 0, and the P.V MFMAs of half 0
+  // between the exps of half 1, so a wave keeps its own matrix pipe busy
+  // while its VALU works (the default form runs QK^T, softmax and P.V of a
+  // tile as three phases and relies on the other waves of the SIMD for
+  // overlap).  The range guard runs per half: a half whose lane sum (16
+  // keys) exceeds 2^lim moves the offsets of its rows exactly as the whole-
+  // tile guard does (a 16-key sum > 2^lim implies a p > 2^(lim-4)), and a
+  // P.V already accumulated for half 0 is rescaled with O and l (its p were
+  // finite).  Same products in the same order per row: results equal the
+  // default form's up to the order of the fp32 row-sum adds.
+  auto tile_split = [&](auto bufc, auto zc) {
+    constexpr int BUF = decltype(bufc)::value;
+    constexpr bool ZL = decltype(zc)::value;
+    const char* base = smem + BUF * 2 * TILEB;
+    f32x16 s0 = f32x16{}, s1 = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const bf16x8 kf = *(const bf16x8*)(base + ka[ks]);
+      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s0, 0, 0, 0);
+    }
+    bf16x8 k1[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) k1[ks] = *(const bf16x8*)(base + ka[ks] + 32 * ROWB);
+    bf16x8 p0[2], p1[2];
+    auto exph = [&](const f32x16& sv, bf16x8 (&pf)[2], auto shc) -> float {
+      constexpr bool shifted = decltype(shc)::value;
+      float r = 0.f;
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        bf16x8 tv;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float x = sv[8 * ss + j];
+          if constexpr (shifted) x -= m_run;
+          const float pv = __builtin_amdgcn_exp2f(x);
+          if (ss == 0 && j == 0) r = pv;
+          else r += pv;
+          tv[j] = (__bf16)pv;
+        }
+        pf[ss] = tv;
+      }
+      return r;
+    };
+    auto pv_half = [&](int kb, const bf16x8 (&pf)[2]) {
+#pragma unroll
+      for (int db = 0; db < NDB; ++db)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const char* p0_ = base + va[db] + (kb * 32 + 16 * ss) * ROWB;
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)LDS_PTR(p0_));
+          const s16x4 hi =
+              __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)LDS_PTR(p0_ + 8 * ROWB));
+          const bf16x8 vf = __builtin_bit_cast(bf16x8, (s16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[ss], o[db], 0, 0, 0);
+        }
+    };
+    auto rowmax = [&](const f32x16& a0, const f32x16* a1) {
+      float mx = fmaxf(a0[0], a0[1]);
+#pragma unroll
+      for (int r = 2; r < 16; r += 2) mx = fmaxf(fmaxf(mx, a0[r]), a0[r + 1]);
+      if (a1) {
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) mx = fmaxf(fmaxf(mx, (*a1)[r]), (*a1)[r + 1]);
+      }
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    };
+    auto move_offset = [&](float mx) {
+      float m_new = m_run;
+      if (m_run == M_UNSET) m_new = fabsf(mx) <= 60.f ? 0.f : mx;
+      else if (mx > m_run + (lim - 5.f)) m_new = mx;
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+      m_run = m_new;
+      lim = m_run == 0.f ? 60.f : THR;
+      limv = m_run == 0.f ? 0x1p60f : 256.0f;
+      zero_off = __builtin_amdgcn_ballot_w64(m_run != 0.f) == 0;
+      l_run *= alpha;
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) o[db] *= alpha;
+    };
+    // QK^T of half 1 beside the exps of half 0
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1[ks], qf[ks], s1, 0, 0, 0);
+    float r0 = exph(s0, p0, std::integral_constant<bool, !ZL>{});
+    if ((__builtin_amdgcn_ballot_w64(!(r0 <= limv)) != 0) || (ZL && !zero_off)) {
+      // rare: the whole tile from raw scores (first tile, or an offset move in half 0)
+      const S2 raw = qk_again(bufc);
+      move_offset(rowmax(raw.v[0], &raw.v[1]));
+      l_run += exph(raw.v[0], p0, std::true_type{});
+      l_run += exph(raw.v[1], p1, std::true_type{});
+      pv_half(0, p0);
+      pv_half(1, p1);
+      return;
+    }
+    l_run += r0;
+    // P.V of half 0 beside the exps of half 1
+    pv_half(0, p0);
+    float r1 = exph(s1, p1, std::integral_constant<bool, !ZL>{});
+    if (__builtin_amdgcn_ballot_w64(!(r1 <= limv)) != 0) {
+      const S2 raw = qk_again(bufc);
+      move_offset(rowmax(raw.v[1], nullptr));
+      r1 = exph(raw.v[1], p1, std::true_type{});
+    }
+    l_run += r1;
+    pv_half(1, p1);
+  };
+
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
@@ -473,12 +588,14 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
     auto run = [&](auto zc, int t0) -> int {
       for (int t = t0; t < nt; t += 2) {
         if (t + 1 < nt) stage(1, t + 1);
-        soft_pv(I0{}, t, qk(I0{}), zc);
+        if ((VAR & 256) && (t + 1) * BKV <= a.nk) tile_split(I0{}, zc);
+        else soft_pv(I0{}, t, qk(I0{}), zc);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (t + 1 >= nt) break;
         if (t + 2 < nt) stage(0, t + 2);
-        soft_pv(I1{}, t + 1, qk(I1{}), zc);
+        if ((VAR & 256) && (t + 2) * BKV <= a.nk) tile_split(I1{}, zc);
+        else soft_pv(I1{}, t + 1, qk(I1{}), zc);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if constexpr (decltype(zc)::value) {
@@ -842,6 +959,12 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
     else if (nw == 8) attn_fwd_kernel<64, 8, 19><<<nwg, 512, 0, s>>>(a);
     else if (g_vggt_attn_variant == 23) attn_fwd_kernel<64, 4, 23><<<nwg, 256, 0, s>>>(a);
     else attn_fwd_kernel<64, 4, 19><<<nwg, 256, 0, s>>>(a);
+    HIP_LAUNCH_CHECK();
+    return VGGT_OK;
+  }
+  if (g_vggt_attn_variant == 289 && D == 64 && nw != 2 && !a.lse) {  // offset-free, split-tile pipelined
+    if (nw == 8) attn_fwd_kernel<64, 8, 289><<<nwg, 512, 0, s>>>(a);
+    else attn_fwd_kernel<64, 4, 289><<<nwg, 256, 0, s>>>(a);
     HIP_LAUNCH_CHECK();
     return VGGT_OK;
   }

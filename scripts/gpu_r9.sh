@@ -48,4 +48,8 @@ if has pmc; then
   timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 GRBM_GUI_ACTIVE --output-format csv -d $P/mops -o run -- $BENCH > "$OUT/mops.log" 2>&1 || exit $?
   python3 scripts/step_pmc.py $P/busy $P/mops --out "$OUT/step_mfma.json" || exit $?
 fi
+
+if has kbench; then
+  step kbench_attn 300 python -u scripts/kbench.py --only attn --attn-waves 8,4 --attn-variants ${ATTN_VARIANTS:-33,289} --rounds 2 --warm-s 2 || exit $?
+fi
 echo "[$(date +%T)] done"
