@@ -62,6 +62,9 @@ const char* vggt_version(void);
 #define VGGT_TUNE_CONV_PF2 4     /* split-bf16 conv gather: 1 two-deep (buffer loads, default), 0 one-deep */
 #define VGGT_TUNE_ATTN16 5       /* 1: D = 64 attention on the 16x16x32 matrix-core form, 0: 32x32x16 (default),
                                     2: 16x16x32 for 4-wave (nq < 4096) launches only */
+#define VGGT_TUNE_LINEAR_ONE_LAUNCH 6 /* vggt_linear_f32_ws split-K: 1 the last split block of a tile combines the
+                                         partials in the same launch (default), 0 a separate reduce launch (same
+                                         fixed summation order: bitwise equal; kept for A/B and tests) */
 /* (knob 6, the persistent GEMM's DMA-placement bits, is retired: its measured-best placement is the only
    one compiled; vggt_tune(6, ...) returns VGGT_ERR_UNSUPPORTED) */
 int vggt_tune(int knob, int value);

@@ -141,6 +141,7 @@ TUNE_ATTN_WAVES = 2
 TUNE_ATTN_VARIANT = 3
 TUNE_CONV_PF2 = 4
 TUNE_ATTN16 = 5
+TUNE_LINEAR_ONE_LAUNCH = 6
 
 
 def tune(knob: int, value: int) -> int:

@@ -24,6 +24,7 @@ int g_vggt_attn_variant = env_or("VGGT_ATTN_VARIANT", 33);
 // (profiles/r6d), frame-only faster (r7b: step 98.9-99.0 -> 98.3 ms)
 int g_vggt_attn16 = env_or("VGGT_ATTN16", 2);
 int g_vggt_conv_pf2 = env_or("VGGT_CONV_PF2", 1);
+int g_vggt_linear_one_launch = env_or("VGGT_LINEAR_ONE_LAUNCH", 1);
 
 extern "C" int vggt_tune(int knob, int value) {
   int prev;
@@ -44,8 +45,9 @@ extern "C" int vggt_tune(int knob, int value) {
     case VGGT_TUNE_ATTN_VARIANT:
       // 0-15: bit combinations of the max-tracking kernel; 19/23: pipelined QK^T;
       // 32/33 (+64 exact scores): offset-free softmax; 161 = 33 on the 16x16x32 MFMA shape (D = 64)
+      // 289 = 33 with the split-tile in-wave pipeline (D = 64)
       if (value < 0 || (value > 15 && value != 19 && value != 23 && value != 32 && value != 33 && value != 96 &&
-                        value != 97 && value != 161))
+                        value != 97 && value != 161 && value != 289))
         return VGGT_ERR_UNSUPPORTED;
       prev = g_vggt_attn_variant;
       g_vggt_attn_variant = value;
@@ -54,6 +56,11 @@ extern "C" int vggt_tune(int knob, int value) {
       if (value < 0 || value > 2) return VGGT_ERR_UNSUPPORTED;
       prev = g_vggt_attn16;
       g_vggt_attn16 = value;
+      return prev;
+    case VGGT_TUNE_LINEAR_ONE_LAUNCH:
+      if (value != 0 && value != 1) return VGGT_ERR_UNSUPPORTED;
+      prev = g_vggt_linear_one_launch;
+      g_vggt_linear_one_launch = value;
       return prev;
     case VGGT_TUNE_CONV_PF2:
       if (value != 0 && value != 1) return VGGT_ERR_UNSUPPORTED;

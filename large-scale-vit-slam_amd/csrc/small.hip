@@ -7,6 +7,7 @@
 #include <stdlib.h>
 
 #include "common.h"
+#include "tune.h"
 
 namespace {
 
@@ -438,7 +439,8 @@ extern "C" int vggt_linear_f32_ws(const float* A, int64_t lda, const float* W, i
   const int kchunk = splits > 1 ? ((K + splits - 1) / splits + 15) / 16 * 16 : K;
   float* part = splits > 1 ? (float*)((char*)ws + cbytes) : nullptr;
   // one launch (last block per tile combines) while the tile words fit
-  unsigned* cnt = (splits > 1 && blocks <= VGGT_LINEAR_F32_WS_COUNTERS) ? (unsigned*)ws : nullptr;
+  unsigned* cnt =
+      (splits > 1 && blocks <= VGGT_LINEAR_F32_WS_COUNTERS && g_vggt_linear_one_launch) ? (unsigned*)ws : nullptr;
   const dim3 grid((N + 63) / 64, gy, splits);
   hipStream_t s = (hipStream_t)stream;
 #define LAUNCH(AI, E) \

@@ -41,13 +41,18 @@ def test_linear_f32(N, M, Nn, K, epi, act):
     assert _rel(out, ref) < 2e-6
 
 
-@pytest.mark.parametrize("M,Nn,K,epi", [(16, 512, 512, 3), (16, 2048, 512, 1), (1, 512, 2048, 2), (130, 1536, 1024, 3),
-                                         (16, 7, 256, 3), (256, 4096, 4096, 1)])
-def test_linear_f32_split_k_one_launch(N, M, Nn, K, epi):
+@pytest.mark.parametrize("M,Nn,K,epi,act", [(16, 512, 512, 3, 0), (16, 2048, 512, 1, 0), (1, 512, 2048, 2, 0),
+                                             (130, 1536, 1024, 3, 0), (16, 7, 256, 3, 0), (256, 4096, 4096, 1, 0),
+                                             (16, 6144, 2048, 3, 1), (16, 512, 1024, 2, 1)])
+def test_linear_f32_split_k_one_launch(N, M, Nn, K, epi, act):
     """Skinny-M split-K (vggt_linear_f32_ws): the last split block of each output
     tile combines the partials in split order in the same launch.  Bitwise
-    run-to-run (fixed order), within fp32 rounding of an fp64 reference, and the
-    scratch's tile counters are left zero for the next call."""
+    run-to-run (fixed order) AND bitwise equal to the two-launch form (partials,
+    then a reduce launch in the same split order; VGGT_TUNE_LINEAR_ONE_LAUNCH 0),
+    within fp32 rounding of an fp64 reference, incl. the SiLU-on-input form
+    (act_in = 1: the camera head's adaLN modulation), and the scratch's tile
+    counters are left zero for the next call."""
+    import torch.nn.functional as F_
     g = torch.Generator(device="cuda").manual_seed(M * Nn + K)
     a = torch.randn(M, K, device="cuda", generator=g)
     w = torch.randn(Nn, K, device="cuda", generator=g) / K ** 0.5
@@ -55,13 +60,19 @@ def test_linear_f32_split_k_one_launch(N, M, Nn, K, epi):
     gam = torch.rand(Nn, device="cuda", generator=g) if epi == 2 else None
     base = torch.randn(M, Nn, device="cuda", generator=g)
     outs = []
-    for _ in range(3):
-        out = base.clone()
-        N.linear_f32(a, w, b, out, epi, gamma=gam)
+    for one in (1, 1, 1, 0):
+        prev = N.tune(N.TUNE_LINEAR_ONE_LAUNCH, one)
+        try:
+            out = base.clone()
+            N.linear_f32(a, w, b, out, epi, act_in=act, gamma=gam)
+        finally:
+            N.tune(N.TUNE_LINEAR_ONE_LAUNCH, prev)
         outs.append(out)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
-    ref = a.double() @ w.double().t() + b.double()
+    assert torch.equal(outs[0], outs[3]), (outs[0] - outs[3]).abs().max()  # one launch == two launches, bitwise
+    x = F_.silu(a.double()) if act else a.double()
+    ref = x @ w.double().t() + b.double()
     if epi == 1:
         ref = F.gelu(ref)
     if epi == 2:
