@@ -56,6 +56,7 @@ class RingCosts:
     t_pause_ungated: float = 1.6
     hop: float = 0.25
     gather: float = 0.5
+    ship: float = 0.3
     source: str = ""
 
     def job_ms(self, kind: str, frames: int, g: int) -> float:
@@ -187,6 +188,11 @@ class RankPlan:
     sizes: Tuple[int, ...] = ()
     policy: str = "with"
     gated: bool = True
+    # align_rank[i]: the rank that runs chunk i's alignment (the same tuple in every
+    # rank's plan); () = the owner (i mod W).  An alignment away from its owner gets
+    # the chunk's core outputs by one point-to-point "ship" (the alignment head's
+    # prefix rows + the camera pose encoding, ~27 MB at 154x518)
+    align_rank: Tuple[int, ...] = ()
 
 
 @dataclass
@@ -221,7 +227,8 @@ def _timeline(jobs: Sequence[Job], lengths, costs: RingCosts, pauses: Sequence[f
 
 
 def simulate(lengths: Sequence[int], W: int, plans: Sequence[RankPlan], costs: RingCosts) -> Prediction:
-    """Predicted sequence time of the ring (chunk i on rank i mod W)."""
+    """Predicted sequence time of the ring: chunk i's core encode on its owner
+    (i mod W), its alignment on plans[*].align_rank[i] (default the owner)."""
     n = len(lengths)
     core_job: Dict[int, Tuple[int, int]] = {}
     for r, pl in enumerate(plans):
@@ -229,21 +236,25 @@ def simulate(lengths: Sequence[int], W: int, plans: Sequence[RankPlan], costs: R
             if kind in ("enc", "core"):
                 for i in g:
                     core_job[i] = (r, j)
+    ar = plans[0].align_rank if plans and plans[0].align_rank else tuple(i % W for i in range(n))
     pauses: List[List[float]] = [[] for _ in range(W)]
     a_s: List[float] = []
     a_e: List[float] = []
     tp = [costs.t_pause if pl.gated else costs.t_pause_ungated for pl in plans]
     for i in range(n):
         r, j = core_job[i]
-        tl = _timeline(plans[r].jobs, lengths, costs, pauses[r], tp[r])
-        s = tl[j]
+        a = ar[i]
+        s = _timeline(plans[r].jobs, lengths, costs, pauses[r], tp[r])[j]
+        if a != r:
+            s += costs.ship
         if i > 0:
-            s = max(s, a_e[-1] + (costs.hop if W > 1 else 0.0))
-        busy = s < tl[-1]  # the rank still has encode work queued at s
+            s = max(s, a_e[-1] + (costs.hop if ar[i - 1] != a else 0.0))
+        tla = _timeline(plans[a].jobs, lengths, costs, pauses[a], tp[a])
+        busy = bool(tla) and s < tla[-1]  # the aligning rank still has encode work queued at s
         if busy:
-            pauses[r].append(s)
+            pauses[a].append(s)
         a_s.append(s)
-        a_e.append(s + ((costs.t_align if plans[r].gated else costs.t_align_ungated) if busy
+        a_e.append(s + ((costs.t_align if plans[a].gated else costs.t_align_ungated) if busy
                         else costs.t_align_alone))
     fin = [(_timeline(pl.jobs, lengths, costs, pauses[r], tp[r]) or [0.0])[-1] for r, pl in enumerate(plans)]
     total = max(max(fin), a_e[-1] if a_e else 0.0) + costs.gather
@@ -255,12 +266,16 @@ _POLICIES = ("with", "lag", "end")
 
 def plan_ring(lengths: Sequence[int], W: int, costs: Optional[RingCosts] = None, cap: int = 3,
               policies: Sequence[str] = _POLICIES, gates: Sequence[bool] = (True, False),
-              sweeps: int = 3) -> Tuple[List[RankPlan], Prediction]:
+              sweeps: int = 3, offload: bool = True) -> Tuple[List[RankPlan], Prediction]:
     """Per-rank plans minimising the predicted sequence time: each rank's
     longest equal-length run is cut into groups of <= cap chunks (every
     composition tried) under each DPT placement policy, gated or not, rank by rank, a few
-    coordinate-descent sweeps from the best uniform choice.  Deterministic, so
-    every rank computes the same plans."""
+    coordinate-descent sweeps from the best uniform choice.  Then (offload)
+    alignments move, one at a time, from the rank that finishes last to the
+    ranks that finish first while the prediction improves: 43 chunks over 8
+    ranks leave two ranks six chunks, and their alignments' gate pauses are
+    what keeps them last.  Deterministic, so every rank computes the same
+    plans."""
     costs = costs or load_costs()
     n = len(lengths)
     owns = [list(range(r, n, W)) for r in range(W)]
@@ -304,7 +319,42 @@ def plan_ring(lengths: Sequence[int], W: int, costs: Optional[RingCosts] = None,
                     sc, choice, pr, changed = s2, trial, p2, True
         if not changed:
             break
-    return build(choice), pr
+    plans = build(choice)
+    if offload and W > 1:
+        plans, pr = _offload(lengths, W, plans, costs, pr)
+    return plans, pr
+
+
+def _offload(lengths, W, plans, costs, pr):
+    """Greedy alignment moves off the last-finishing rank (see plan_ring)."""
+    n = len(lengths)
+    ar = list(i % W for i in range(n))
+
+    def with_ar(a):
+        for pl in plans:
+            pl.align_rank = tuple(a)
+        return simulate(lengths, W, plans, costs)
+
+    best = with_ar(ar)
+    key = lambda p: (round(p.total_ms, 6), round(max(p.rank_finish), 6), round(sum(p.rank_finish), 6))  # noqa: E731
+    for _ in range(n):
+        R = max(range(W), key=lambda r: best.rank_finish[r])
+        targets = sorted(range(W), key=lambda r: best.rank_finish[r])[:3]
+        cand = None
+        for i in [i for i in range(n) if ar[i] == R]:
+            for q in targets:
+                if q == R:
+                    continue
+                trial = list(ar)
+                trial[i] = q
+                p2 = with_ar(trial)
+                if key(p2) < key(best) and (cand is None or key(p2) < key(cand[1])):
+                    cand = (trial, p2)
+        if cand is None:
+            break
+        ar, best = cand
+    with_ar(ar)
+    return plans, best
 
 
 def _fit(c: Tuple[int, ...], m: int, cap: int) -> Tuple[int, ...]:

@@ -21,10 +21,6 @@ step() {  # step NAME SECONDS CMD...
   return $rc
 }
 has() { [ "$WHAT" = all ] || [[ ",$WHAT," == *",$1,"* ]]; }
-if has tests; then
-  step pytest 900 python -u -m pytest ${TESTS:-tests/test_gpu_pipeline.py tests/test_gpu_gate.py tests/test_gpu_ring.py tests/test_gpu_fullsize.py} \
-    -x -v -s --timeout 400 --timeout-method thread ${KEXPR:+-k "$KEXPR"} || exit $?
-fi
 if has seq; then
   step c3 400 python -u bench.py --config 3 --steps 3 --warmup 2 --no-cpu-baseline || exit $?
   grep '^{' "$OUT/c3.out" | tail -1 > "$OUT/c3.json"
@@ -51,5 +47,9 @@ fi
 
 if has kbench; then
   step kbench_attn 300 python -u scripts/kbench.py --only attn --attn-waves 8,4 --attn-variants ${ATTN_VARIANTS:-33,289} --rounds 2 --warm-s 2 || exit $?
+fi
+if has tests; then
+  step pytest 900 python -u -m pytest ${TESTS:-tests/test_gpu_pipeline.py tests/test_gpu_gate.py tests/test_gpu_ring.py tests/test_gpu_fullsize.py} \
+    --maxfail=5 -v -s --timeout 400 --timeout-method thread ${KEXPR:+-k "$KEXPR"} || exit $?
 fi
 echo "[$(date +%T)] done"

@@ -233,18 +233,19 @@ def test_pose_error_budget(model, golden, run):
     torch.cuda.synchronize()
     p = f"{run}_bf16_"
     sizes = [len(c) - 1 for c in chunks]
-    cs_h = ctx["chunk_sim3_alignment_enc"].cpu().double()
-    fs_h = list(torch.split(ctx["frame_se3_alignment_enc"].cpu().double(), sizes, dim=1))
-    cs_r = t(g[p + "chunk_sim3"]).double()
-    fs_r = list(torch.split(t(g[p + "frame_se3"]).double(), sizes, dim=1))
-    pe_h = [x.cpu().double() for x in ctx["pose_enc"]]
-    pe_r = [t(g[p + f"pose_enc{i}"]).double() for i in range(len(chunks))]
+    # fp32 throughout, as the reference composes (featureAligned_vggt.py:104: autocast off)
+    cs_h = ctx["chunk_sim3_alignment_enc"].cpu().float()
+    fs_h = list(torch.split(ctx["frame_se3_alignment_enc"].cpu().float(), sizes, dim=1))
+    cs_r = t(g[p + "chunk_sim3"]).float()
+    fs_r = list(torch.split(t(g[p + "frame_se3"]).float(), sizes, dim=1))
+    pe_h = [x.cpu().float() for x in ctx["pose_enc"]]
+    pe_r = [t(g[p + f"pose_enc{i}"]).float() for i in range(len(chunks))]
 
     def compose(i, cs, fs, prev):
         S = len(chunks[i])
         o = ov if S > ov else S - 1
-        gt0 = fa_gt_poses(run, i, S)[:, 0].double() if (use_gt and i > 0) else None
-        return O.compose_poses(cs[:, i:i + 1], fs, feeds[i]["pose_enc"].double(), prev if i > 0 else None, gt0, o,
+        gt0 = fa_gt_poses(run, i, S)[:, 0].float() if (use_gt and i > 0) else None
+        return O.compose_poses(cs[:, i:i + 1], fs, feeds[i]["pose_enc"].float(), prev if i > 0 else None, gt0, o,
                                (H, W))[0]
 
     rows = []
