@@ -213,6 +213,7 @@ class ChunkPipeline:
         # rank's encode is gated; these restrict its choices
         self.plan_policies = tuple(os.environ.get("VGGT_RING_POLICIES", "with,lag,end").split(","))
         self.plan_gates = (True, False)
+        self.plan_offload = os.environ.get("VGGT_RING_OFFLOAD", "1") != "0"
         self._local = None
         self.prediction = None
 
@@ -295,26 +296,43 @@ class ChunkPipeline:
         ops = [dist.P2POp(dist.isend, t, dst, group=self.group) for t in ts]
         return dist.batch_isend_irecv(ops), ts
 
-    def _irecv(self, src: int, shapes: Dict[str, tuple]):
+    def _irecv(self, src: int, shapes: Dict[str, tuple], group=None):
         out = {k: torch.empty(shp, device=self._comm_device, dtype=torch.float32) for k, shp in shapes.items()}
-        ops = [dist.P2POp(dist.irecv, t, src, group=self.group) for t in out.values()]
+        ops = [dist.P2POp(dist.irecv, t, src, group=self.group if group is None else group) for t in out.values()]
         return dist.batch_isend_irecv(ops), out
 
-    def _p2p_warmup(self):
+    def _p2p_warmup(self, baton_pairs=None, ship_pairs=()):
         """Create the ring's point-to-point communicators up front (RCCL builds
         a pair's communicator on its first send/recv, blocking both hosts until
         the peer joins -- inside the timed loop that would stall the enqueue of
-        the next encode)."""
-        if self.world == 1 or self.__dict__.get("_p2p_ready"):
+        the next encode).  baton_pairs: (src, dst) rank pairs the batons travel
+        (default r -> r + 1); ship_pairs: those that carry offloaded
+        alignments' inputs, on their own process group (so a ship and a baton
+        between the same two ranks are never matched against each other)."""
+        if self.world == 1:
             return
         W, r = self.world, self.rank
-        a = torch.zeros(1, device=self._comm_device)
-        b = torch.zeros(1, device=self._comm_device)
-        ops = [dist.P2POp(dist.isend, a, (r + 1) % W, group=self.group),
-               dist.P2POp(dist.irecv, b, (r - 1) % W, group=self.group)]
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
-        self._p2p_ready = True
+        if baton_pairs is None:
+            baton_pairs = [(q, (q + 1) % W) for q in range(W)]
+        key = (tuple(sorted(set(baton_pairs))), tuple(sorted(set(ship_pairs))))
+        done = self.__dict__.setdefault("_p2p_done", set())
+        if ship_pairs and self.__dict__.get("_ship_group") is None:
+            ranks = dist.get_process_group_ranks(self.group) if self.group is not None else list(range(W))
+            self._ship_group = dist.new_group(ranks=ranks, backend=dist.get_backend(self.group))
+        for pairs, grp in ((key[0], self.group), (key[1], self.__dict__.get("_ship_group"))):
+            if not pairs or (pairs, id(grp)) in done:
+                continue
+            ops, keep = [], []
+            for src, dst in pairs:  # the same canonical order on every rank
+                if src == dst or r not in (src, dst):
+                    continue
+                t = torch.zeros(1, device=self._comm_device)
+                keep.append(t)
+                ops.append(dist.P2POp(dist.isend if r == src else dist.irecv, t, dst if r == src else src, group=grp))
+            if ops:
+                for w in dist.batch_isend_irecv(ops):
+                    w.wait()
+            done.add((pairs, id(grp)))
 
     # ---------------------------------------------------------------- run
     @torch.no_grad()
@@ -329,6 +347,7 @@ class ChunkPipeline:
         chunks = generate_chunks(Nf, "chunk_overlap", chunk_width, num_overlap)
         keys = ["overlap_tokens", "pose_enc"] + (["memory_tokens"] if memory_shape is not None else [])
         self.align_events = []
+        dense: Dict[int, dict] = {}
         if self.world == 1 and not self.overlap_align:
             mine = self._run_local(images, chunks, num_overlap, keys, memory_shape, B)
         elif ((self.reserve_cus > 0 or self.short_workgroups or self.gate_encode) and self.device is not None
@@ -337,13 +356,13 @@ class ChunkPipeline:
             cur = torch.cuda.current_stream(self.device)
             enc_stream.wait_stream(cur)
             with torch.cuda.stream(enc_stream):
-                mine = self._run_ring(images, chunks, num_overlap, keys, token_dims, memory_shape, B)
+                mine, dense = self._run_ring(images, chunks, num_overlap, keys, token_dims, memory_shape, B)
             cur.wait_stream(enc_stream)
-            for v in mine.values():
+            for v in list(mine.values()) + list(dense.values()):
                 _record_stream(v, cur)
         else:
-            mine = self._run_ring(images, chunks, num_overlap, keys, token_dims, memory_shape, B)
-        return self._gather(mine, chunks, num_overlap, B)
+            mine, dense = self._run_ring(images, chunks, num_overlap, keys, token_dims, memory_shape, B)
+        return self._gather(mine, dense, chunks, num_overlap, B)
 
     def _encode_stream(self):
         """The ring's encode stream: a dedicated non-blocking HIP stream, or one
@@ -382,7 +401,12 @@ class ChunkPipeline:
         policies = tuple(self.plan_policies) if defer else ("with",)
         gates = tuple(self.plan_gates) if (cuda and self.gate_encode) else (False,)
         legacy = os.environ.get("VGGT_RING_PLAN", "auto") == "legacy"
-        key = (tuple(lengths), W, cap, policies, gates, legacy)
+        # alignments may run away from their chunk's owner when the model can ship
+        # their inputs (the alignment head's prefix rows: FeatureAlignedVGGT in
+        # no-grad inference with VGGT_ALIGN_PREFIX on)
+        offload = self.plan_offload and W > 1 and hasattr(self.model, "ship_spec") and \
+            self.model.ship_spec(images.shape[0], lengths[0], *images.shape[-2:]) is not None
+        key = (tuple(lengths), W, cap, policies, gates, legacy, offload)
         cache = self.__dict__.setdefault("_plan_cache", {})
         if key not in cache:
             costs = SC.load_costs()
@@ -392,9 +416,10 @@ class ChunkPipeline:
                     pl.gated = gates[0]
                 pred = SC.simulate(lengths, W, plans, costs)
             else:
-                plans, pred = SC.plan_ring(lengths, W, costs, cap, policies, gates)
+                plans, pred = SC.plan_ring(lengths, W, costs, cap, policies, gates, offload=offload)
             cache[key] = (plans, pred)
         self.prediction = cache[key][1]
+        self._last_plans = cache[key][0]
         return cache[key][0]
 
     def _encode(self, images, chunks, g: List[int], frames, dense: bool = True):
@@ -484,16 +509,17 @@ class ChunkPipeline:
             gate = self._gate = EncodeGate(self.device)
         return gate
 
-    def _run_ring(self, images, chunks, num_overlap, keys, token_dims, memory_shape, B) -> Dict[int, dict]:
-        """Rank r owns chunks r, r + W, ...  Its encode stream runs the plan's
-        jobs (dist/schedule.py: groups of its own chunks, the DPT heads with
-        the encode or later); each alignment runs on a high-priority side
-        stream that waits (device-side) for its chunk's core encode and for the
-        baton from rank i - 1, and posts the baton to rank i + 1 (isend) as
-        soon as it is done -- the host never blocks on a peer, and the compute
-        stream keeps encoding while a baton is in flight.  Depth maps whose
-        DPT head ran after the alignment are scaled by the chunk Sim(3) at the
-        end (``scale_dense``).
+    def _run_ring(self, images, chunks, num_overlap, keys, token_dims, memory_shape, B):
+        """Rank r encodes chunks r, r + W, ... (its encode stream runs the
+        plan's jobs, dist/schedule.py: groups of its own chunks, the DPT heads
+        with the encode or later) and aligns the chunks the plan gives it
+        (``align_rank``: its own, minus those shipped to a less loaded rank,
+        plus those shipped to it).  Each alignment runs on a high-priority
+        side stream that waits (device-side) for the chunk's core encode -- or
+        for its shipped inputs -- and for the baton from the rank that aligned
+        chunk i - 1, and posts the baton to the rank that aligns chunk i + 1
+        (isend) as soon as it is done: the host never blocks on a peer, and the
+        compute stream keeps encoding while a baton is in flight.
 
         The baton's irecv is posted on the side stream BEFORE the side stream
         waits for the chunk's encode: RCCL orders its communication stream
@@ -504,16 +530,22 @@ class ChunkPipeline:
 
         W == 1 (``overlap_align``): the same schedule on one GPU with the baton
         kept on the device -- chunk i aligns on the side stream while the next
-        encode job runs on the compute stream."""
+        encode job runs on the compute stream.
+
+        Returns (summaries of the chunks aligned here, raw DPT outputs of own
+        chunks whose depth was not scaled by their alignment: a DPT head that
+        ran after it, or an alignment shipped away -- scaled in ``_gather``)."""
         from .schedule import enqueue_order
         W, r = self.world, self.rank
         n = len(chunks)
         P1, C = token_dims
         cuda = self.device is not None and torch.device(self.device).type == "cuda"
-        self._p2p_warmup()
-        own = list(range(r, n, W))
         plan = self.plans(chunks, images, cuda)[r]
-        self.enqueue_log = []  # ("job", kind, chunks) / ("align", i): the host's issue order (tests)
+        ar = plan.align_rank or tuple(i % W for i in range(n))
+        self._p2p_warmup([(ar[i - 1], ar[i]) for i in range(1, n) if ar[i - 1] != ar[i]],
+                         [(i % W, ar[i]) for i in range(n) if ar[i] != i % W])
+        own = list(range(r, n, W))
+        self.enqueue_log = []  # ("job", kind, chunks) / ("ship", i) / ("align", i): the host's issue order (tests)
         side = main = None
         if cuda:
             # the alignment's own GEMMs: persistent when the encode is gated (the
@@ -525,6 +557,8 @@ class ChunkPipeline:
         ready: Dict[int, object] = {}
         held: Dict[tuple, dict] = {}  # batched core results waiting for their DPT job
         dense: Dict[int, dict] = {}
+        sends = []
+        hw = tuple(images.shape[-2:])
 
         def run_job(j):
             kind, g = plan.jobs[j]
@@ -548,48 +582,68 @@ class ChunkPipeline:
             for i in g:
                 encs[i] = out[i]
                 ready[i] = ev
+                if kind == "enc" and ar[i] != r and "depth" in out[i]:
+                    dense[i] = {k: out[i][k] for k in ("depth", "depth_conf") if k in out[i]}
+
+        def ship(i):
+            """Chunk i's alignment inputs to the rank that aligns it (in chunk order on
+            both ends, on the ship group; RCCL: after the core encode on this stream)."""
+            self.enqueue_log.append(("ship", i))
+            enc = encs.pop(i)
+            ready.pop(i, None)
+            cd = self._comm_device
+            ts = [t.contiguous().to(cd) for t in self.model.ship_payload(enc).values()]
+            ops = [dist.P2POp(dist.isend, t, ar[i], group=self._ship_group) for t in ts]
+            sends.append((dist.batch_isend_irecv(ops), ts))
 
         mine: Dict[int, dict] = {}
-        sends = []
         gate_ctx = contextlib.nullcontext()
         if gate is not None:
             from ..runtime import gated
             gate_ctx = gated(main, gate)
         with gate_ctx:
-            for kind, arg in enqueue_order(plan, own):
+            for kind, arg in enqueue_order(plan, own, r):
                 if kind == "job":
                     run_job(arg)
+                elif kind == "ship":
+                    ship(arg[0])
                 else:
                     self.enqueue_log.append(("align", arg[0]))
-                    self._align_one(arg[0], encs, ready, side, cuda, chunks, num_overlap, keys, B, P1, C,
-                                    memory_shape, mine, sends, gate)
+                    self._align_one(arg[0], ar, encs, ready, side, cuda, chunks, num_overlap, keys, B, P1, C,
+                                    memory_shape, mine, sends, gate, hw)
         for works, _ in sends:
             for w in works:
                 w.wait()
         if cuda:
             main.wait_stream(side)
-            for v in mine.values():
+            for v in list(mine.values()) + list(dense.values()):
                 _record_stream(v, main)
-        for i, d in dense.items():  # featureAligned_vggt.py:171 for the deferred depth maps
-            mine[i].update(self.model.scale_dense(d, mine[i]["chunk_sim3"]))
-        return mine
+        return mine, dense
 
-    def _align_one(self, i, encs, ready, side, cuda, chunks, num_overlap, keys, B, P1, C, memory_shape, mine,
-                   sends, gate) -> None:
-        W, n = self.world, len(chunks)
-        enc = encs.pop(i)
+    def _align_one(self, i, ar, encs, ready, side, cuda, chunks, num_overlap, keys, B, P1, C, memory_shape, mine,
+                   sends, gate, hw) -> None:
+        W, n, r = self.world, len(chunks), self.rank
+        S = len(chunks[i])
         with (torch.cuda.stream(side) if cuda else contextlib.nullcontext()):
             ctx = None
             works = ()
-            if i > 0 and W > 1:
+            if i > 0 and ar[i - 1] != r:
                 Sp = len(chunks[i - 1])
-                works, ctx_in = self._irecv((i - 1) % W, self._baton_shapes(
+                works, ctx_in = self._irecv(ar[i - 1], self._baton_shapes(
                     B, Sp, _overlap_of(Sp, num_overlap), P1, C, memory_shape))
-            if cuda:
-                side.wait_event(ready.pop(i))
-                _record_stream(enc, side)
+            if i % W == r:
+                enc = encs.pop(i)
+                if cuda:
+                    side.wait_event(ready.pop(i))
+                    _record_stream(enc, side)
+            else:  # shipped here by its owner
+                spec = self.model.ship_spec(B, S, *hw)
+                sw, got = self._irecv(i % W, spec, group=self._ship_group)
+                for w in sw:
+                    w.wait()
+                enc = self.model.enc_from_ship({k: v.to(self.device) for k, v in got.items()}, B, S, *hw)
             if i > 0:
-                if W > 1:
+                if ar[i - 1] != r:
                     for w in works:
                         w.wait()  # RCCL: the side stream waits; gloo: the host does
                     ctx_in = {k: v.to(self.device) for k, v in ctx_in.items()}  # no-op unless host-staged
@@ -612,11 +666,11 @@ class ChunkPipeline:
                 if gate is not None:
                     gate.end(side)  # also on an error: a held gate would stall every later encode
             if i + 1 < n:
-                if W > 1:
-                    sends.append(self._isend(pred, (i + 1) % W, keys))
+                if ar[i + 1] != r:
+                    sends.append(self._isend(pred, ar[i + 1], keys))
                 else:
                     self._local = {k: (pred[k][-1] if isinstance(pred[k], list) else pred[k]) for k in keys}
-            mine[i] = self._summary(pred, len(chunks[i]))
+            mine[i] = self._summary(pred, S)
 
     def _tick(self):
         """A timing event on the current stream (``time_align`` on a HIP device), else None."""
@@ -635,18 +689,22 @@ class ChunkPipeline:
             out.append(a.elapsed_time(b))
         return out
 
-    def _gather(self, mine: Dict[int, dict], chunks: List[List[int]], num_overlap: int, B: int) -> Optional[dict]:
+    def _gather(self, mine: Dict[int, dict], dense: Dict[int, dict], chunks: List[List[int]], num_overlap: int,
+                B: int) -> Optional[dict]:
         """Every chunk's small outputs (pose encodings, chunk Sim(3), frame
-        SE(3); depth maps with ``gather_dense``) on every rank: ONE fixed-shape
-        ``all_gather_into_tensor`` per kind (RCCL over xGMI).  Rank r's block
-        holds its own chunks r, r + W, ... in slot order, each padded to the
-        longest chunk; chunk i is slot i // W of rank i % W's block."""
+        SE(3)) on every rank through ONE fixed-shape ``all_gather_into_tensor``
+        (RCCL over xGMI), then the depth maps of chunks whose DPT head ran after
+        their alignment (or whose alignment ran on another rank) scaled by their
+        chunk Sim(3) on the owner (featureAligned_vggt.py:171), and with
+        ``gather_dense`` the depth maps through a second one."""
         n = len(chunks)
         W = self.world
         if W > 1:
-            per_chunk = self._all_gather_chunks(mine, chunks, B)
+            per_chunk = self._all_gather_chunks(mine, dense, chunks, B)
         else:
             per_chunk = mine
+            for i, d in dense.items():
+                per_chunk[i].update(self.model.scale_dense(d, per_chunk[i]["chunk_sim3"]))
         ov = num_overlap
         out = {
             "pose_enc": torch.cat([per_chunk[i]["pose_enc"][:, (ov if i > 0 else 0):] for i in range(n)], 1),
@@ -658,26 +716,27 @@ class ChunkPipeline:
             out["depth_conf"] = torch.cat([per_chunk[i]["depth_conf"][:, (ov if i > 0 else 0):] for i in range(n)], 1)
         return out
 
-    def _all_gather_chunks(self, mine: Dict[int, dict], chunks: List[List[int]], B: int) -> Dict[int, dict]:
+    def _all_gather_chunks(self, mine: Dict[int, dict], dense: Dict[int, dict], chunks: List[List[int]],
+                           B: int) -> Dict[int, dict]:
+        """Rank q's block of the small gather holds the chunks it aligned
+        (align_rank) in chain order, each padded to the longest chunk; the
+        dense gather holds the chunks it owns (i mod W), whose depth it has."""
         W, r = self.world, self.rank
         n = len(chunks)
-        slots = (n + W - 1) // W
+        plan = self._last_plans[r]  # the plans this run executed
+        ar = plan.align_rank or tuple(i % W for i in range(n))
+        aligned = [[i for i in range(n) if ar[i] == q] for q in range(W)]
+        slot_of = {i: (q, j) for q in range(W) for j, i in enumerate(aligned[q])}
+        slots = max(1, max(len(a) for a in aligned))
         smax = max(len(c) for c in chunks)
         dev = self._comm_device
-        # small outputs, per slot: [has_depth, depth H, depth W, pose_enc B*smax*9, chunk_sim3 B*8,
-        # frame_se3 B*(smax-1)*7]; the DPT maps are 14*(H//14) x 14*(W//14), so their size travels too
-        seg = (3, B * smax * 9, B * 8, B * (smax - 1) * 7)
+        # small outputs, per slot: [pose_enc B*smax*9, chunk_sim3 B*8, frame_se3 B*(smax-1)*7]
+        seg = (0, B * smax * 9, B * 8, B * (smax - 1) * 7)
         per = sum(seg)
         buf = torch.zeros(slots, per, device=dev, dtype=torch.float32)
-        for j in range(slots):
-            i = r + j * W
-            if i >= n:
-                continue
+        for j, i in enumerate(aligned[r]):
             S, m = len(chunks[i]), mine[i]
             o = seg[0]
-            if self.gather_dense and "depth" in m:
-                buf[j, 0] = 1.0
-                buf[j, 1], buf[j, 2] = float(m["depth"].shape[2]), float(m["depth"].shape[3])
             buf[j, o:o + B * S * 9] = m["pose_enc"].reshape(-1).to(dev)
             o += seg[1]
             buf[j, o:o + B * 8] = m["chunk_sim3"].reshape(-1).to(dev)
@@ -689,7 +748,8 @@ class ChunkPipeline:
         allb = allb.to(out_dev)
         per_chunk: Dict[int, dict] = {}
         for i in range(n):
-            row = allb[(i % W) * slots + i // W]
+            q, j = slot_of[i]
+            row = allb[q * slots + j]
             S = len(chunks[i])
             o = seg[0]
             per_chunk[i] = {"pose_enc": row[o:o + B * S * 9].view(B, S, 9)}
@@ -697,24 +757,38 @@ class ChunkPipeline:
             per_chunk[i]["chunk_sim3"] = row[o:o + B * 8].view(B, 1, 8)
             o += seg[2]
             per_chunk[i]["frame_se3"] = row[o:o + B * (S - 1) * 7].view(B, S - 1, 7)
-        # every rank sees every chunk's flag, so all agree on the dense collective
-        # (one device-to-host copy of the flag column)
-        flags = allb[:, :3].cpu()
-        if all(float(flags[(i % W) * slots + i // W, 0]) > 0 for i in range(n)):
-            H, Wd = int(flags[0, 1]), int(flags[0, 2])  # chunk 0 = rank 0's slot 0
+        # this rank's own depth maps: scaled by their alignment already, or now (deferred / shipped)
+        own = list(range(r, n, W))
+        local = {}
+        for i in own:
+            if i in dense:
+                local[i] = self.model.scale_dense(dense[i], per_chunk[i]["chunk_sim3"].to(out_dev))
+            elif i in mine and "depth" in mine[i]:
+                local[i] = {"depth": mine[i]["depth"], "depth_conf": mine[i]["depth_conf"]}
+        # the dense collective only when every chunk has a depth map and it was asked for:
+        # one flag per rank (all agree), the DPT map size with it (14*(H//14) x 14*(W//14))
+        hwf = torch.zeros(1, 3, device=dev, dtype=torch.float32)
+        if self.gather_dense and all(i in local for i in own):
+            hwf[0, 0] = 1.0
+            if own:
+                hwf[0, 1], hwf[0, 2] = float(local[own[0]]["depth"].shape[2]), float(local[own[0]]["depth"].shape[3])
+        allf = torch.empty(W, 3, device=dev, dtype=torch.float32)
+        dist.all_gather_into_tensor(allf, hwf, group=self.group)
+        allf = allf.cpu()
+        if bool((allf[:, 0] > 0).all()):
+            H, Wd = int(allf[0, 1]), int(allf[0, 2])  # rank 0 owns chunk 0
             pix = H * Wd
-            d = torch.zeros(slots, 2, B * smax * pix, device=dev, dtype=torch.float32)
-            for j in range(slots):
-                i = r + j * W
-                if i < n:
-                    S = len(chunks[i])
-                    d[j, 0, :B * S * pix] = mine[i]["depth"].reshape(-1).to(dev)
-                    d[j, 1, :B * S * pix] = mine[i]["depth_conf"].reshape(-1).to(dev)
-            alld = torch.empty(W * slots, 2, B * smax * pix, device=dev, dtype=torch.float32)
+            oslots = (n + W - 1) // W
+            d = torch.zeros(oslots, 2, B * smax * pix, device=dev, dtype=torch.float32)
+            for j, i in enumerate(own):
+                S = len(chunks[i])
+                d[j, 0, :B * S * pix] = local[i]["depth"].reshape(-1).to(dev)
+                d[j, 1, :B * S * pix] = local[i]["depth_conf"].reshape(-1).to(dev)
+            alld = torch.empty(W * oslots, 2, B * smax * pix, device=dev, dtype=torch.float32)
             dist.all_gather_into_tensor(alld, d, group=self.group)
             alld = alld.to(out_dev)
             for i in range(n):
-                row = alld[(i % W) * slots + i // W]
+                row = alld[(i % W) * oslots + i // W]
                 S = len(chunks[i])
                 per_chunk[i]["depth"] = row[0, :B * S * pix].view(B, S, H, Wd, 1)
                 per_chunk[i]["depth_conf"] = row[1, :B * S * pix].view(B, S, H, Wd)

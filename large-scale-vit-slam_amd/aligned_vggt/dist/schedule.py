@@ -385,29 +385,44 @@ def legacy_plans(lengths: Sequence[int], W: int, cap: int = 3) -> List[RankPlan]
     return plans
 
 
-def enqueue_order(plan: RankPlan, own: Sequence[int]) -> List[Tuple[str, Tuple[int, ...]]]:
+def enqueue_order(plan: RankPlan, own: Sequence[int], rank: Optional[int] = None
+                  ) -> List[Tuple[str, Tuple[int, ...]]]:
     """The host-side order in which the ring issues this rank's work: its jobs
-    in plan order, and alignment i right after the job FOLLOWING the one that
-    produced chunk i's core (one job of look-ahead keeps the encode stream
-    fed while the host waits on a host-blocking baton; over RCCL nothing
-    blocks).  Returns ("job", chunks) / ("align", (i,)) entries."""
+    in plan order; after a job, the "ship" of each chunk in it whose alignment
+    runs on another rank; and alignment i right after the job FOLLOWING the
+    last job that produced a core of one of this rank's chunks <= i (one job of
+    look-ahead keeps the encode stream fed while the host waits on a
+    host-blocking baton; over RCCL nothing blocks).  Every own chunk < i is
+    thus encoded and shipped before alignment i is issued, so a host-blocking
+    baton can never wait on this rank's own later work.  Returns ("job", (j,)),
+    ("ship", (i,)) and ("align", (i,)) entries."""
     jobs = plan.jobs
+    ar = plan.align_rank
     core_at = {}
     for j, (kind, g) in enumerate(jobs):
         if kind in ("enc", "core"):
             for i in g:
                 core_at[i] = j
+    aligns = list(own) if not ar else [i for i in range(len(ar)) if ar[i] == rank]
+    own_sorted = sorted(own)
     out: List[Tuple[str, Tuple[int, ...]]] = []
     issued = -1
-    for i in own:
-        need = min(core_at[i] + 1, len(jobs) - 1)
+
+    def issue_to(need):
+        nonlocal issued
         while issued < need:
             issued += 1
             out.append(("job", issued))
+            kind, g = jobs[issued]
+            if ar and kind in ("enc", "core"):
+                out.extend(("ship", (c,)) for c in g if ar[c] != rank)
+
+    for i in aligns:
+        prior = [core_at[c] for c in own_sorted if c <= i]
+        if prior:
+            issue_to(min(max(prior) + 1, len(jobs) - 1))
         out.append(("align", (i,)))
-    while issued < len(jobs) - 1:
-        issued += 1
-        out.append(("job", issued))
+    issue_to(len(jobs) - 1)
     return out
 
 

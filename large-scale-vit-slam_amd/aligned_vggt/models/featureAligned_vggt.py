@@ -160,6 +160,41 @@ class FeatureAlignedVGGT(nn.Module, PyTorchModelHubMixin):
         B = enc["depth"].shape[0]
         return {"depth": N.scale_(enc["depth"], chunk_sim3_enc[..., -1].reshape(B)), "depth_conf": enc["depth_conf"]}
 
+    # --- moving an alignment to another rank (dist/schedule.py offload): what align_chunk
+    # reads from an encode in no-grad inference is the alignment head's prefix rows and
+    # the camera-head pose encoding; the receiver rebuilds a stub encode around them
+    def ship_spec(self, B: int, S: int, H: int, W: int):
+        """{name: shape} (fp32) of ``ship_payload`` for a chunk of S frames of H x W, or
+        None when align_chunk needs more than that (training, VGGT_ALIGN_PREFIX=0)."""
+        if not _ALIGN_PREFIX or self.alignment_head.training or self.alignment_head.trainable():
+            return None
+        ps = self.aggregator.patch_size
+        ps = ps[0] if isinstance(ps, (tuple, list)) else int(ps)
+        P = (H // ps) * (W // ps) + int(self.aggregator.patch_start_idx)
+        spec = {"ah_prep": (B, S * (P + 1), self.embed_dim)}
+        if self.camera_head is not None:
+            spec["cam_pose_enc"] = (B, S, 9)
+        return spec
+
+    def ship_payload(self, enc: dict) -> dict:
+        out = {"ah_prep": enc["ah_prep"]}
+        if self.camera_head is not None:
+            out["cam_pose_enc"] = enc["cam_pose_enc"]
+        return out
+
+    def enc_from_ship(self, t: dict, B: int, S: int, H: int, W: int) -> dict:
+        """A stub encode for align_chunk: the shipped tensors, and zero-stride views
+        standing in for the frames and the last token layer (only their shapes and
+        device are read: align_chunk's prefix path, featureAligned_vggt.py:84-143)."""
+        dev = t["ah_prep"].device
+        P1 = t["ah_prep"].shape[1] // S
+        one = torch.zeros(1, device=dev)
+        enc = {"images": one.expand(B, S, 3, H, W), "tokens": [one.expand(B, S, P1 - 1, 2 * self.embed_dim)],
+               "patch_start_idx": int(self.aggregator.patch_start_idx), "ah_prep": t["ah_prep"]}
+        if "cam_pose_enc" in t:
+            enc["cam_pose_enc"] = t["cam_pose_enc"]
+        return enc
+
     def prepare_align(self, enc: dict, num_overlap: int, context: dict = None, gt_poses: torch.Tensor = None) -> None:
         """Everything align_chunk may do that synchronises the device, done
         ahead of it: with VGGT_ALIGN_GRAPH=1 the first chunk of each shape

@@ -39,8 +39,8 @@ def _worker(rank, world, port, Nf, w, ov, q, group=None, policies=None):
         # the host's issue order against the plan's (dist/schedule.py enqueue_order)
         chunks = generate_chunks(Nf, "chunk_overlap", w, ov)
         plan = pipe.plans(chunks, images, False)[rank]
-        expect = [("job",) + tuple(plan.jobs[a]) if k == "job" else ("align", a[0])
-                  for k, a in enqueue_order(plan, list(range(rank, len(chunks), world)))]
+        expect = [("job",) + tuple(plan.jobs[a]) if k == "job" else (k, a[0])
+                  for k, a in enqueue_order(plan, list(range(rank, len(chunks), world)), rank)]
         res = {k: v.numpy().copy() for k, v in out.items()}
         res["_order_ok"] = pipe.enqueue_log == expect
         res["_policies"] = sorted({kind for kind, _ in plan.jobs})

@@ -30,6 +30,15 @@ class ToyAlignModel:
         enc["depth_conf"] = images[:, :, 1] + 1
         return enc
 
+    def ship_spec(self, B, S, H, W):
+        return {"tok": (B, S, P1, C)}
+
+    def ship_payload(self, enc):
+        return {"tok": enc["tok"]}
+
+    def enc_from_ship(self, t, B, S, H, W):
+        return {"images": torch.zeros(1).expand(B, S, 3, H, W), "tok": t["tok"]}
+
     def scale_dense(self, enc, sim3):
         B = enc["depth"].shape[0]
         return {"depth": enc["depth"] * sim3[..., -1].view(B, 1, 1, 1, 1), "depth_conf": enc["depth_conf"]}
