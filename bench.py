@@ -459,7 +459,8 @@ def bench_full(args, world, rank, dev):
         dt = t.item()
     recurrence = ring_model = None
     if args.workload == "sequence" and os.environ.get("VGGT_RECURRENCE_PROBE", "1") != "0":
-        recurrence = _recurrence_probe(pipe, step, n_chunks_step, dt / args.steps * 1e3, world)
+        recurrence = _recurrence_probe(pipe, step, lambda: pipe.prepare(seq, S, ov), n_chunks_step,
+                                       dt / args.steps * 1e3, world)
         if world == 1:
             ring_model = _ring_model(model, pipe, seq, S, ov, recurrence, dt / args.steps * 1e3)
     if world > 1:
@@ -482,7 +483,7 @@ def bench_full(args, world, rank, dev):
               flush=True)
 
 
-def _recurrence_probe(pipe, step, n_chunks, t1_ms, world):
+def _recurrence_probe(pipe, step, prepare, n_chunks, t1_ms, world):
     """The alignment recurrence's critical path: chunk i's
     alignment needs chunk i-1's post-head tokens, so with W ranks a sequence
     takes at least n_chunks x t_align (+ W-1 .. n-1 baton hops) whatever the
@@ -520,6 +521,7 @@ def _recurrence_probe(pipe, step, n_chunks, t1_ms, world):
             pipe.gate_encode = gate
         keep_gates = pipe.plan_gates
         pipe.plan_gates = (pipe.gate_encode,)  # the mode's gate on every rank, not the planner's choice
+        prepare()  # the planner's host-side search outside the timed call
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         step()

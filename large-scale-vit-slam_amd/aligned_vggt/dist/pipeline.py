@@ -364,6 +364,17 @@ class ChunkPipeline:
             mine, dense = self._run_ring(images, chunks, num_overlap, keys, token_dims, memory_shape, B)
         return self._gather(mine, dense, chunks, num_overlap, B)
 
+    def prepare(self, images: torch.Tensor, chunk_width: int, num_overlap: int) -> None:
+        """Compute (and cache) the ring's plans for this sequence shape ahead of
+        ``run`` -- the planner's search is a few seconds of host time
+        (dist/schedule.py), which the first ``run`` of a configuration would
+        otherwise spend before its first launch."""
+        if self.world == 1 and not self.overlap_align:
+            return
+        chunks = generate_chunks(images.shape[1], "chunk_overlap", chunk_width, num_overlap)
+        cuda = self.device is not None and torch.device(self.device).type == "cuda"
+        self.plans(chunks, images, cuda)
+
     def _encode_stream(self):
         """The ring's encode stream: a dedicated non-blocking HIP stream, or one
         masked off `reserve_cus` CUs, registered with the library
@@ -419,8 +430,13 @@ class ChunkPipeline:
                 plans, pred = SC.plan_ring(lengths, W, costs, cap, policies, gates, offload=offload)
             cache[key] = (plans, pred)
         self.prediction = cache[key][1]
-        self._last_plans = cache[key][0]
-        return cache[key][0]
+        plans = cache[key][0]
+        ov = self.__dict__.get("align_rank_override")
+        if ov is not None:  # tests: a fixed alignment placement instead of the planner's
+            import dataclasses
+            plans = [dataclasses.replace(pl, align_rank=tuple(ov)) for pl in plans]
+        self._last_plans = plans
+        return plans
 
     def _encode(self, images, chunks, g: List[int], frames, dense: bool = True):
         """One encode job over the chunks in g: (per-chunk results, the batched result)."""

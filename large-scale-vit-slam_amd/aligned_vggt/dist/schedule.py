@@ -117,12 +117,12 @@ def compositions(n: int, cap: int) -> List[Tuple[int, ...]]:
 def candidate_sizes(n: int, cap: int, full_upto: int = 8) -> List[Tuple[int, ...]]:
     """Group-size sequences tried for a run of n chunks: every composition
     for short runs (a W >= 4 rank owns <= 11 of 43 chunks); for long runs
-    (W = 1, 2) a head of up to 3 chunks in any composition, a uniform middle
-    of groups of g, and a tail of up to 3 chunks in any composition."""
+    (W = 1, 2) a head of up to 2 chunks in any composition, a uniform middle
+    of groups of g, and a tail of up to 2 chunks in any composition."""
     if n <= full_upto:
         return compositions(n, cap)
     out = set()
-    ends = [c for k in range(0, 4) for c in compositions(k, cap)]
+    ends = [c for k in range(0, 3) for c in compositions(k, cap)]
     for head in ends:
         for tail in ends:
             mid = n - sum(head) - sum(tail)
@@ -266,7 +266,7 @@ _POLICIES = ("with", "lag", "end")
 
 def plan_ring(lengths: Sequence[int], W: int, costs: Optional[RingCosts] = None, cap: int = 3,
               policies: Sequence[str] = _POLICIES, gates: Sequence[bool] = (True, False),
-              sweeps: int = 3, offload: bool = True) -> Tuple[List[RankPlan], Prediction]:
+              sweeps: int = 2, offload: bool = True) -> Tuple[List[RankPlan], Prediction]:
     """Per-rank plans minimising the predicted sequence time: each rank's
     longest equal-length run is cut into groups of <= cap chunks (every
     composition tried) under each DPT placement policy, gated or not, rank by rank, a few
@@ -293,8 +293,9 @@ def plan_ring(lengths: Sequence[int], W: int, costs: Optional[RingCosts] = None,
         pr = simulate(lengths, W, build(choice), costs)
         return (round(pr.total_ms, 6), round(sum(pr.rank_finish), 6)), pr
 
-    # start: the best choice applied to every rank alike (by pattern of the largest rank)
-    best = None
+    # starts: for each DPT policy, the best choice applied to every rank alike (by the
+    # pattern of the largest rank); each start is refined by coordinate descent
+    uniform = {}
     for c, p, gt in options[0]:
         choice = []
         for r in range(W):
@@ -303,22 +304,27 @@ def plan_ring(lengths: Sequence[int], W: int, costs: Optional[RingCosts] = None,
             cc = c if mine == m else _fit(c, mine, cap)
             choice.append((cc, p, gt))
         sc, pr = score(choice)
+        if p not in uniform or sc < uniform[p][0]:
+            uniform[p] = (sc, choice, pr)
+    best = None
+    for p in sorted(uniform):
+        sc, choice, pr = uniform[p]
+        for _ in range(sweeps):
+            changed = False
+            for r in range(W):
+                for opt in options[r]:
+                    if opt == choice[r]:
+                        continue
+                    trial = list(choice)
+                    trial[r] = opt
+                    s2, p2 = score(trial)
+                    if s2 < sc:
+                        sc, choice, pr, changed = s2, trial, p2, True
+            if not changed:
+                break
         if best is None or sc < best[0]:
             best = (sc, choice, pr)
     sc, choice, pr = best
-    for _ in range(sweeps):
-        changed = False
-        for r in range(W):
-            for opt in options[r]:
-                if opt == choice[r]:
-                    continue
-                trial = list(choice)
-                trial[r] = opt
-                s2, p2 = score(trial)
-                if s2 < sc:
-                    sc, choice, pr, changed = s2, trial, p2, True
-        if not changed:
-            break
     plans = build(choice)
     if offload and W > 1:
         plans, pr = _offload(lengths, W, plans, costs, pr)
@@ -341,7 +347,11 @@ def _offload(lengths, W, plans, costs, pr):
         R = max(range(W), key=lambda r: best.rank_finish[r])
         targets = sorted(range(W), key=lambda r: best.rank_finish[r])[:3]
         cand = None
-        for i in [i for i in range(n) if ar[i] == R]:
+        # the last-finishing rank's alignments, and the chain's tail (alignments that start
+        # after the first rank has run out of encode work run there at their alone speed)
+        idle_from = min(best.rank_finish)
+        movable = [i for i in range(n) if ar[i] == R or best.align_start[i] >= idle_from]
+        for i in movable:
             for q in targets:
                 if q == R:
                     continue
@@ -432,8 +442,11 @@ def predict_scaling(lengths: Sequence[int], costs: RingCosts, worlds=(1, 2, 4, 8
     out = {}
     for W in worlds:
         plans, pr = plan_ring(lengths, W, costs)
+        _, pr_no = plan_ring(lengths, W, costs, offload=False) if W > 1 else (None, pr)
         leg = simulate(lengths, W, legacy_plans(lengths, W), costs)
-        out[str(W)] = {"T_ms": round(pr.total_ms, 1), "T_ms_round4_schedule": round(leg.total_ms, 1),
+        moved = [i for i, a in enumerate(plans[0].align_rank) if a != i % W] if plans[0].align_rank else []
+        out[str(W)] = {"T_ms": round(pr.total_ms, 1), "T_ms_no_offload": round(pr_no.total_ms, 1),
+                       "T_ms_round4_schedule": round(leg.total_ms, 1), "alignments_moved": moved,
                        "plans": [{"groups": [list(g) for k, g in pl.jobs if k in ("enc", "core")],
                                   "policy": pl.policy, "gated": pl.gated} for pl in plans[:min(W, 3)]]}
     return out

@@ -26,7 +26,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, Nf, w, ov, q, group=None, policies=None):
+def _worker(rank, world, port, Nf, w, ov, q, group=None, policies=None, shift=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -35,6 +35,9 @@ def _worker(rank, world, port, Nf, w, ov, q, group=None, policies=None):
         pipe = ChunkPipeline(ToyAlignModel(), device=torch.device("cpu"), gather_dense=True, encode_group=group)
         if policies is not None:
             pipe.plan_policies = policies
+        if shift is not None:  # every alignment on another rank than its chunk's owner
+            n = len(generate_chunks(Nf, "chunk_overlap", w, ov))
+            pipe.align_rank_override = tuple((i + shift) % world for i in range(n))
         out = pipe.run(images, w, ov, token_dims=(P1, C), memory_shape=(2, NMEM, DEC))
         # the host's issue order against the plan's (dist/schedule.py enqueue_order)
         chunks = generate_chunks(Nf, "chunk_overlap", w, ov)
@@ -44,6 +47,7 @@ def _worker(rank, world, port, Nf, w, ov, q, group=None, policies=None):
         res = {k: v.numpy().copy() for k, v in out.items()}
         res["_order_ok"] = pipe.enqueue_log == expect
         res["_policies"] = sorted({kind for kind, _ in plan.jobs})
+        res["_ships"] = sum(1 for e in pipe.enqueue_log if e[0] == "ship")
         # the end-of-sequence all-gather leaves the merged outputs on every rank
         q.put((rank, res))  # by value: the worker may exit first
     finally:
@@ -82,12 +86,24 @@ def test_pipeline_plan_policies(world, policy):
         assert got["_policies"] == (["enc"] if policy == "with" else ["core", "dense"]), (r, got["_policies"])
 
 
-def _run_world(world, Nf, w, ov, group, policies):
+@pytest.mark.parametrize("world,Nf,w,ov,shift,policy", [(2, 44, 6, 2, 1, "end"), (3, 60, 6, 2, 1, "with"),
+                                                      (3, 60, 6, 2, 2, "lag"), (4, 40, 8, 3, 1, "end")])
+def test_pipeline_offloaded_alignments(world, Nf, w, ov, shift, policy):
+    """Alignments away from their chunk's owner (dist/schedule.py offload): the
+    owner ships the alignment's inputs on the ship process group, batons go
+    between the aligning ranks, the depth maps are scaled by the owner after
+    the small gather -- bitwise the loop's results, in the plan's issue order."""
+    outs = _run_world(world, Nf, w, ov, None, (policy,), shift)
+    assert sum(o["_ships"] for o in outs.values()) > 0
+
+
+def _run_world(world, Nf, w, ov, group, policies, shift=None):
     ref = _sequential(Nf, w, ov)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, Nf, w, ov, q, group, policies)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, Nf, w, ov, q, group, policies, shift))
+             for r in range(world)]
     for p in procs:
         p.start()
     outs = dict(q.get(timeout=180) for _ in range(world))

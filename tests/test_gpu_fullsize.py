@@ -164,8 +164,9 @@ def test_alignment_head_at_configs2_size(cuda):
     assert o0.shape == (1, ov + 1, 1375, 1024) and cs1.shape == (1, 1, 8) and fs1.shape == (1, 15, 7)
     for k in ("cs0", "cs1"):  # the north star on the chunk Sim(3)
         assert e[k] < 1e-3, (k, e)
-    # about 2x the values measured on MI355X (round 5)
-    bars = {"fs0": 3e-3, "fs1": 3e-3, "mem0": 1e-2, "mem1": 1e-2, "ov0": 2e-2, "ov1": 2e-2}
+    # about 2x the values measured on MI355X (round 5: fs 8.3e-4 / 6.6e-4, memory 2.8e-3 / 2.6e-3, the
+    # post-head overlap tokens 4.0e-5 / 5.5e-5 -- the oracle's own bf16-vs-fp32 spread is 2.9e-3 there)
+    bars = {"fs0": 2e-3, "fs1": 2e-3, "mem0": 6e-3, "mem1": 6e-3, "ov0": 1.5e-4, "ov1": 1.5e-4}
     for k, bar in bars.items():
         assert e[k] < bar, (k, e[k], bar)
 
@@ -208,7 +209,15 @@ def test_configs2_sequence_518_reduced_depth(cuda):
     spread = {k: (_quat_rel if k == "pose_quat" else _rel)(rf[k], rb[k]) for k in g}
     _report("configs[2] 2 x 16 x 518^2", e, spread)
     assert e["chunk_sim3"] < 1e-3, e  # north star
-    bars = {"frame_se3": 3e-3, "depth": 2e-3, "depth_conf": 1e-4, "memory": 1e-2, "overlap": 2e-2,
-            "pose_T": 1e-1, "pose_quat": 5e-2, "pose_fov": 5e-2}
+    # 2x the values measured on MI355X (round 5: frame_se3 8.3e-4, depth 1.4e-4, conf 3.1e-6, memory
+    # 2.8e-3, overlap 3.1e-3, pose T 8.9e-2 / quat 1.5e-2 / FoV 9.6e-3).  The poses go through the
+    # random-init camera head, whose translations amplify the bf16 tier's token error (the camera
+    # head itself matches the oracle to 1e-4 on identical tokens, test_gpu_model.py
+    # test_heads_fp32_tier_tight; the oracle's own bf16-vs-fp32 pose spread here: T 7.8e-2, quat
+    # 1.2e-2, FoV 1.1e-2), so the poses are ALSO held within 1.5x of that spread
+    bars = {"frame_se3": 2e-3, "depth": 3e-4, "depth_conf": 1e-5, "memory": 6e-3, "overlap": 7e-3,
+            "pose_T": 0.18, "pose_quat": 3e-2, "pose_fov": 2e-2}
     for k, bar in bars.items():
         assert e[k] < bar, (k, e[k], bar)
+    for k in ("pose_T", "pose_quat", "pose_fov"):
+        assert e[k] < 1.5 * spread[k], (k, e[k], spread[k])

@@ -184,8 +184,12 @@ def test_feature_aligned_composition_vs_reference(model, golden, run):
             assert v < 1e-6, (k, e)
         elif k.startswith("q"):
             assert v < 1e-5, (k, e)
-        elif k.startswith(("T", "depth", "pts")):
-            assert v < 5e-3, (k, e)
+        elif k.startswith(("T", "pts")):
+            # composed translations / points: 2x the measured (<= 1.7e-3 after four chained chunks;
+            # the budget is test_pose_error_budget: head error x chain, composition 1e-7)
+            assert v < 3.5e-3, (k, e)
+        elif k.startswith("depth"):
+            assert v < 1e-3, (k, e)  # = the chunk scale's error (measured <= 5e-4)
         else:
             assert v < 3e-3, (k, e)
 
@@ -275,3 +279,12 @@ def test_pose_error_budget(model, golden, run):
     for r in rows:
         # depth = depth_raw x scale: its error IS the scale's (fp32 round-off aside)
         assert abs(r["depth"] - r["in_scale"]) < 1e-5 + 1e-3 * r["in_scale"], r
+        # every input's share is bounded by the total it composes to (no hidden term)
+        assert max(r["T_from_chunk_sim3"], r["T_from_frame_se3"], r["T_from_context"]) < 2.5 * r["T_total"] + 1e-5, r
+    # measured on MI355X (round 5): a first chunk (no context) composes to T 4.2e-4 .. 5.0e-4 -- within the
+    # north star's 1e-3 -- and the error grows along the chain only through the context (the previous
+    # chunk's poses via the Markley mean): 1.3e-3 .. 1.6e-3 after four chunks; bars 2x measured
+    assert rows[0]["T_total"] < 1e-3, rows[0]
+    assert all(r["T_total"] < 3.5e-3 for r in rows), rows
+    if use_gt:
+        assert all(r["T_from_context"] == 0.0 for r in rows)  # chunk_gt: the GT pose replaces the context

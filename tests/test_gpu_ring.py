@@ -36,7 +36,7 @@ def _model():
     return m.cuda().eval()
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, shift=None):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "large-scale-vit-slam_amd")]
@@ -49,6 +49,10 @@ def _worker(rank, world, port, q):
         m = _model()
         imgs = synthetic_images(1, N_FRAMES, H, W, seed=4).cuda()
         pipe = ChunkPipeline(m, device=torch.device("cuda"), gather_dense=True, time_align=True)
+        if shift is not None:  # every alignment away from its owner: the shipped prefix rows path
+            from aligned_vggt.utils.data import generate_chunks
+            n = len(generate_chunks(N_FRAMES, "chunk_overlap", W_CHUNK, OV))
+            pipe.align_rank_override = tuple((i + shift) % world for i in range(n))
         P1 = 6 + (H // 14) * (W // 14)
         out = pipe.run(imgs, W_CHUNK, OV, token_dims=(P1, 1024), memory_shape=(1, 8, 512))
         torch.cuda.synchronize()
@@ -57,7 +61,11 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_ring_two_ranks_real_model_matches_loop():
+@pytest.mark.parametrize("shift", [None, 1])
+def test_ring_two_ranks_real_model_matches_loop(shift):
+    """shift 1: every chunk's alignment runs on the other rank (its encode's
+    alignment-head prefix rows and camera pose encoding shipped there, the
+    depth maps scaled by the owner after the gather)."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     import torch.multiprocessing as mp
@@ -72,7 +80,7 @@ def test_ring_two_ranks_real_model_matches_loop():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, shift)) for r in range(2)]
     for p in procs:
         p.start()
     got = [q.get(timeout=240) for _ in range(2)]

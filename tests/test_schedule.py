@@ -49,7 +49,7 @@ def test_candidate_sizes_cover_the_run():
     for n in (1, 5, 6, 9, 42):
         cs = SC.candidate_sizes(n, 3)
         assert cs and all(sum(c) == n and max(c) <= 3 for c in cs), n
-    assert (3,) * 14 in SC.candidate_sizes(42, 3)
+    assert (3,) * 14 in SC.candidate_sizes(42, 3) and (2,) + (3,) * 13 + (1,) in SC.candidate_sizes(42, 3)
 
 
 def test_enqueue_order_lookahead():
