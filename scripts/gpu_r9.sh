@@ -29,6 +29,10 @@ if has c4; then
   step c4 400 python -u bench.py --config 4 --steps 3 --warmup 2 --no-cpu-baseline || exit $?
   grep '^{' "$OUT/c4.out" | tail -1 > "$OUT/c4.json"
 fi
+if has c0; then
+  step c0 300 python -u bench.py --config 0 --steps 10 --warmup 3 || exit $?
+  grep '^{' "$OUT/c0.out" | tail -1 > "$OUT/c0.json"
+fi
 if has head; then
   step headline 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline || exit $?
   grep '^{' "$OUT/headline.out" | tail -1 > "$OUT/headline.json"
