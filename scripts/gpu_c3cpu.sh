@@ -16,15 +16,18 @@ CPID=$!
 if [ "${GPU_WORK:-1}" = 1 ]; then
   P=/tmp/prof_c3cpu
   echo "[$(date +%T)] trace headline"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $P/agg -o run -- python3 bench.py --steps 5 --warmup 2 \
-    --no-cpu-baseline > "$OUT/prof.log" 2>&1 && python3 scripts/prof_summary.py $P/agg/run_results.db \
+  VGGT_MFMA_PROBE=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $P/agg -o run -- python3 bench.py --steps 5 \
+    --warmup 2 --no-cpu-baseline > "$OUT/prof.log" 2>&1 && python3 scripts/prof_summary.py $P/agg/run_results.db \
     > "$OUT/aggregator_kernels.md" && grep '^{' "$OUT/prof.log" | tail -1 > "$OUT/bench_under_rocprof.json"
-  echo "[$(date +%T)] configs[2]"
-  timeout -k 10 400 python3 -u bench.py --config 2 --steps 3 --warmup 2 --no-cpu-baseline > "$OUT/c2.out" 2>&1 \
-    && grep '^{' "$OUT/c2.out" | tail -1 > "$OUT/c2.json"
-  echo "[$(date +%T)] chunk"
-  timeout -k 10 300 python3 -u bench.py --workload chunk --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/chunk.out" 2>&1 \
-    && grep '^{' "$OUT/chunk.out" | tail -1 > "$OUT/chunk.json"
+  echo "[$(date +%T)] train"
+  timeout -k 10 300 python3 -u bench.py --workload train --steps 10 --warmup 3 > "$OUT/train.out" 2>&1 \
+    && grep '^{' "$OUT/train.out" | tail -1 > "$OUT/train.json"
+  echo "[$(date +%T)] attention anatomy"
+  CMD="python3 scripts/kbench.py --only attn --attn-waves 8 --attn-variants 33 --reps 8 --warm-s 1"
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES --output-format csv -d $P/p1 -o run -- $CMD > "$OUT/anat1.log" 2>&1 \
+    && timeout -s KILL 120 rocprofv3 --pmc SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_LDS --output-format csv -d $P/p2 -o run -- $CMD > "$OUT/anat2.log" 2>&1 \
+    && timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d $P/p3 -o run -- $CMD > "$OUT/anat3.log" 2>&1 \
+    && python3 scripts/pmc_anatomy.py $P/p1 $P/p2 $P/p3 --kernel attn_fwd_kernel > "$OUT/attn_anatomy.md" 2>&1
 fi
 echo "[$(date +%T)] waiting for the CPU sequence"
 wait $CPID
