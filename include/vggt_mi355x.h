@@ -65,6 +65,11 @@ const char* vggt_version(void);
 #define VGGT_TUNE_LINEAR_ONE_LAUNCH 6 /* vggt_linear_f32_ws split-K: 1 the last split block of a tile combines the
                                          partials in the same launch (default), 0 a separate reduce launch (same
                                          fixed summation order: bitwise equal; kept for A/B and tests) */
+#define VGGT_TUNE_LINEAR_SPLIT_K 7 /* vggt_linear_f32_ws split-K: split while each split keeps at least this many
+                                      k (power of two, 16..4096; default 128).  Changes the fp32 summation order */
+#define VGGT_TUNE_LINEAR_WK 8 /* vggt_linear_f32_ws with M <= 64: 0 the split-K form above, else the k range
+                                 (power of two, 64..4096; default 64) each wave of an in-workgroup split keeps (2..16 waves on
+                                 16 columns, partials summed in LDS: no scratch, no counters) */
 /* (knob 6, the persistent GEMM's DMA-placement bits, is retired: its measured-best placement is the only
    one compiled; vggt_tune(6, ...) returns VGGT_ERR_UNSUPPORTED) */
 int vggt_tune(int knob, int value);
@@ -120,6 +125,22 @@ int vggt_gemm_qkv(const void* A, int64_t lda, const void* W, int64_t ldw, const 
                   void* out, int64_t ldo, const float* qw, const float* qb, const float* kw, const float* kb, float eps,
                   int rope_mode, const int32_t* pos, int period, const float* cos_tab, const float* sin_tab,
                   int tab_len, void* stream);
+
+/*
+ * The same fused epilogue on the separate projections of a cross attention:
+ * out[M, N] = bf16(A . W^T + bias) with the FIRST H*D columns normalised
+ * (weights nw/nb [D], NULL = no norm) and rotated (rope_mode/pos/period as
+ * above; row m takes position pos[m % period]) and, for N = 2*H*D, the
+ * second block stored as is.  N = H*D: a q projection (+ q_norm + RoPE);
+ * N = 2*H*D: a packed kv projection (+ k_norm + RoPE on k).  Replaces the
+ * q / kv Linears + vggt_headnorm_rope pair of the alignment head's temporal
+ * blocks (CrossAttention, alignment_head.py:369-380): bitwise the same
+ * values, one HBM pass fewer.  Shape rules as vggt_gemm_qkv.
+ */
+int vggt_gemm_headnorm(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int M, int N, int H,
+                       int D, int K, void* out, int64_t ldo, const float* nw, const float* nb, float eps, int rope_mode,
+                       const int32_t* pos, int period, const float* cos_tab, const float* sin_tab, int tab_len,
+                       void* stream);
 
 /*
  * Row LayerNorm over C (fp32 statistics): y = (x-mean)/sqrt(var+eps)*w + b.
@@ -247,13 +268,15 @@ int vggt_layernorm_grouped(const void* x, int in_dtype, int64_t ldx, const float
 int vggt_linear_f32(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, int M, int N, int K,
                     int act_in, int epi, float* out, int64_t ldo, const float* gamma, void* stream);
 /* Same with a caller-provided scratch (device, >= VGGT_LINEAR_F32_WS_COUNTERS * 4 +
- * 16 * roundup(M,64) * N * 4 bytes to allow the maximum split): skinny-M calls are
- * split along K into up to 16 deterministic partial sums combined in a fixed order
+ * VGGT_LINEAR_F32_MAX_SPLITS * roundup(M,64) * N * 4 bytes to allow the maximum split;
+ * a smaller one caps the split): skinny-M calls are
+ * split along K into up to VGGT_LINEAR_F32_MAX_SPLITS deterministic partial sums combined in a fixed order
  * (camera head trunk, alignment decoder: M = 16 frames) by the last split block of
  * each output tile, in the same launch.  The scratch's first
  * VGGT_LINEAR_F32_WS_COUNTERS words are per-tile counters: zero-fill them before a
  * scratch's first use; every call leaves them zero.  ws == NULL: no split. */
 #define VGGT_LINEAR_F32_WS_COUNTERS 1024
+#define VGGT_LINEAR_F32_MAX_SPLITS 32
 int vggt_linear_f32_ws(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, int M, int N, int K,
                        int act_in, int epi, float* out, int64_t ldo, const float* gamma, void* ws, size_t ws_bytes,
                        void* stream);

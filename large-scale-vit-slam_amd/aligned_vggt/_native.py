@@ -34,6 +34,8 @@ _SIGS = {
     "vggt_gemm_bf16": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _vp, _i64, _vp, _vp, _i64, _vp],
     "vggt_gemm_qkv": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _vp, _i64, _vp, _vp, _vp, _vp, _f, _i, _vp, _i, _vp,
                       _vp, _i, _vp],
+    "vggt_gemm_headnorm": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _i, _vp, _i64, _vp, _vp, _f, _i, _vp, _i, _vp,
+                           _vp, _i, _vp],
     "vggt_layernorm": [_vp, _i, _i64, _vp, _vp, _f, _i, _i, _vp, _i, _i64, _vp],
     "vggt_resid_add_layernorm": [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _f, _i, _i, _vp, _i64, _vp],
     "vggt_headnorm_rope": [_vp, _i64, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _i, _vp, _vp, _i, _vp],
@@ -142,6 +144,8 @@ TUNE_ATTN_VARIANT = 3
 TUNE_CONV_PF2 = 4
 TUNE_ATTN16 = 5
 TUNE_LINEAR_ONE_LAUNCH = 6
+TUNE_LINEAR_SPLIT_K = 7
+TUNE_LINEAR_WK = 8
 
 
 def tune(knob: int, value: int) -> int:
@@ -269,6 +273,23 @@ def gemm_qkv(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out: torch.Te
     rc = lib().vggt_gemm_qkv(_p(a), _ld(a), _p(w), _ld(w), _p(bias), M, H, D, K, _p(out), _ld(out), _p(qw), _p(qb),
                              _p(kw), _p(kb), float(eps), mode, _p(pos), period, _p(cos), _p(sin), tab, _stream())
     _check(rc, "vggt_gemm_qkv")
+    return out
+
+
+def gemm_headnorm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, out: torch.Tensor, H: int, D: int, nw=None,
+                  nb=None, eps: float = 0.0, mode: int = ROPE_NONE, pos=None, period: int = 1, cos=None,
+                  sin=None) -> torch.Tensor:
+    """q (N = H*D) or packed kv (N = 2*H*D) projection with the per-head norm +
+    RoPE of the first H*D columns in the epilogue (vggt_gemm_headnorm)."""
+    _dev(a, "gemm_headnorm")
+    M, K = a.shape
+    N_ = w.shape[0]
+    assert a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.shape[1] == K and N_ in (H * D, 2 * H * D)
+    assert out.shape[0] == M and out.shape[1] == N_ and out.dtype == torch.bfloat16
+    tab = cos.shape[0] if cos is not None else 0
+    rc = lib().vggt_gemm_headnorm(_p(a), _ld(a), _p(w), _ld(w), _p(bias), M, N_, H, D, K, _p(out), _ld(out), _p(nw),
+                                  _p(nb), float(eps), mode, _p(pos), period, _p(cos), _p(sin), tab, _stream())
+    _check(rc, "vggt_gemm_headnorm")
     return out
 
 
@@ -411,9 +432,9 @@ def linear_f32(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], o
     M, K = a.shape
     N_ = w.shape[0]
     assert a.dtype == torch.float32 and w.dtype == torch.float32 and w.shape[1] == K and out.shape == (M, N_)
-    # split-K scratch for skinny M: the zeroed per-tile counter words, then at most 16
-    # splits of a 64-row-padded [M, N] fp32 slab
-    need = LINEAR_F32_WS_COUNTERS + 16 * ((M + 63) // 64) * 64 * N_
+    # split-K scratch for skinny M: the zeroed per-tile counter words, then at most
+    # LINEAR_F32_MAX_SPLITS splits of a 64-row-padded [M, N] fp32 slab
+    need = LINEAR_F32_WS_COUNTERS + LINEAR_F32_MAX_SPLITS * ((M + 63) // 64) * 64 * N_
     ws = _split_ws(a.device, need) if M <= 256 else None
     rc = lib().vggt_linear_f32_ws(_p(a), _ld(a), _p(w), _ld(w), _p(bias), M, N_, K, act_in, epi, _p(out), _ld(out),
                                   _p(gamma), _p(ws), 0 if ws is None else ws.numel() * 4, _stream())
@@ -439,6 +460,7 @@ def _stream_key(device) -> tuple:
 
 
 LINEAR_F32_WS_COUNTERS = 1024  # include/vggt_mi355x.h VGGT_LINEAR_F32_WS_COUNTERS
+LINEAR_F32_MAX_SPLITS = 32  # VGGT_LINEAR_F32_MAX_SPLITS
 
 
 def _split_ws(device, n_floats: int) -> torch.Tensor:

@@ -15,6 +15,7 @@ cross_attention.py:66-67 is a no-op), pre-LN block with LayerScale
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Optional
 
 import torch
@@ -24,6 +25,10 @@ from .. import _native as N
 from ..backbone.layers import Attention, LayerScale, Mlp
 from ..runtime import Workspace, _pkey, pack_linear
 from .. import autograd as AG
+
+# the temporal blocks' q_norm / k_norm + RoPE in the q and kv GEMM epilogues
+# (vggt_gemm_headnorm); VGGT_FUSED_HEADNORM=0: the GEMMs, then vggt_headnorm_rope
+_FUSED_HEADNORM = os.environ.get("VGGT_FUSED_HEADNORM", "1") != "0"
 
 
 class CrossAttention(nn.Module):
@@ -117,14 +122,19 @@ class CrossAttentionBlock(nn.Module):
         N.layernorm(ysrc, self.norm3.weight, self.norm3.bias, self.norm3.eps, yn)
         wq, bq = pack_linear(self.attn.q)
         q = ws.buf("ca_q", Mx, C, torch.bfloat16)
-        N.gemm_bf16(xn, wq, bq, q, N.EPI_BF16)
         wkv, bkv = self.attn.packed_kv()
         kv = ws.buf("ca_kv", My, 2 * C, torch.bfloat16)
-        N.gemm_bf16(yn, wkv, bkv, kv, N.EPI_BF16)
         mode = N.ROPE_1D if self.attn.rope is not None else N.ROPE_NONE
-        for buf, which, rp in ((q, "q", rope_q), (kv, "k", rope_k)):
+        fused = _FUSED_HEADNORM and D in (64, 128) and C % 128 == 0 and xn.shape[1] % 32 == 0
+        for a_, w_, b_, buf, which, rp in ((xn, wq, bq, q, "q", rope_q), (yn, wkv, bkv, kv, "k", rope_k)):
             w, b, eps = self._qk_norm(which)
-            if w is not None or mode != N.ROPE_NONE:
+            extra = w is not None or mode != N.ROPE_NONE
+            if fused and extra:
+                N.gemm_headnorm(a_, w_, b_, buf, H, D, w, b, eps, mode, rp[0] if mode else None,
+                                rp[0].numel() if mode else 1, rp[1] if mode else None, rp[2] if mode else None)
+                continue
+            N.gemm_bf16(a_, w_, b_, buf, N.EPI_BF16)
+            if extra:
                 N.headnorm_rope(buf, 0, H, D, w, b, eps, mode, rp[0] if mode else None,
                                 rp[0].numel() if mode else 1, rp[1] if mode else None, rp[2] if mode else None)
         ao = ws.buf("ca_ao", Mx, C, torch.bfloat16)

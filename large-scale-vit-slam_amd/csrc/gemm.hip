@@ -44,6 +44,9 @@ struct Epi {
   int rope_mode, period, tab_len;
   const int32_t* pos;
   const float *cs, *sn;
+  // leading column blocks that are normalised (+ RoPE): 2 = q and k of a fused
+  // qkv row; 1 = the first block only (vggt_gemm_headnorm: a q, or the k of a kv)
+  int nreg = 2;
 };
 
 constexpr int EPI_QKNORM_D64 = 16, EPI_QKNORM_D128 = 17;  // internal epilogue ids
@@ -117,8 +120,8 @@ __device__ __forceinline__ void write_tile(const char* Cs, int m0, int n0, int M
     const float* nb = region ? ep.kb : ep.qb;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      nwv[j] = (region < 2 && nw) ? nw[e0 + j] : 1.f;
-      nbv[j] = (region < 2 && nb) ? nb[e0 + j] : 0.f;
+      nwv[j] = (region < ep.nreg && nw) ? nw[e0 + j] : 1.f;
+      nbv[j] = (region < ep.nreg && nb) ? nb[e0 + j] : 0.f;
     }
     if (!tcs) {
       tcs = ep.cs;
@@ -148,7 +151,7 @@ __device__ __forceinline__ void write_tile(const char* Cs, int m0, int n0, int M
       constexpr int D = EPI == EPI_QKNORM_D64 ? 64 : 128;
       constexpr int LPH = D / 8;  // lanes per head (consecutive: ch is the low index)
       const int region = n / ep.hd;  // 0 q, 1 k, 2 v
-      if (region >= 2) {
+      if (region >= ep.nreg) {
         *(uint4*)((bf16_t*)ep.out + (int64_t)m * ep.ldo + n) = cv;
         continue;
       }
@@ -1832,13 +1835,16 @@ extern "C" int vggt_gemm_bf16_gelu_pre(const void* A, int64_t lda, const void* W
   return gemm_impl(A, lda, W, ldw, bias, M, N, K, VGGT_EPI_GELU_BF16, out, ldo, nullptr, (float*)pre, ldp, stream);
 }
 
-extern "C" int vggt_gemm_qkv(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int M, int H,
-                             int D, int K, void* out, int64_t ldo, const float* qw, const float* qb, const float* kw,
-                             const float* kb, float eps, int rope_mode, const int32_t* pos, int period,
-                             const float* cos_tab, const float* sin_tab, int tab_len, void* stream) {
-  const int hd = H * D, N = 3 * hd;
+namespace {
+// the fused-epilogue GEMM of vggt_gemm_qkv (N = 3 hd, nreg = 2) and vggt_gemm_headnorm
+// (N = hd or 2 hd, nreg = 1)
+int qkv_impl(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int M, int H, int D, int K,
+             void* out, int64_t ldo, const float* qw, const float* qb, const float* kw, const float* kb, float eps,
+             int rope_mode, const int32_t* pos, int period, const float* cos_tab, const float* sin_tab, int tab_len,
+             void* stream, int N, int nreg) {
+  const int hd = H * D;
   if (M <= 0 || H <= 0 || K <= 0 || K % 32 || (D != 64 && D != 128) || hd % 128) return VGGT_ERR_SHAPE;
-  if ((qw == nullptr) != (kw == nullptr)) return VGGT_ERR_UNSUPPORTED;
+  if (nreg == 2 && (qw == nullptr) != (kw == nullptr)) return VGGT_ERR_UNSUPPORTED;
   if (rope_mode != VGGT_ROPE_NONE && rope_mode != VGGT_ROPE_2D && rope_mode != VGGT_ROPE_1D) return VGGT_ERR_UNSUPPORTED;
   if (rope_mode != VGGT_ROPE_NONE && (!pos || !cos_tab || !sin_tab || period <= 0 || tab_len <= 0))
     return VGGT_ERR_SHAPE;
@@ -1846,7 +1852,7 @@ extern "C" int vggt_gemm_qkv(const void* A, int64_t lda, const void* W, int64_t 
       ((uintptr_t)out & 15) || (rope_mode != VGGT_ROPE_NONE && (((uintptr_t)cos_tab | (uintptr_t)sin_tab) & 15)))
     return VGGT_ERR_ALIGN;
   Epi ep{bias, out, ldo, nullptr, nullptr, 0, qw, qb, kw, kb, eps, hd, rope_mode, period, tab_len, pos, cos_tab,
-         sin_tab};
+         sin_tab, nreg};
   hipStream_t s = (hipStream_t)stream;
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* w = (const bf16_t*)W;
@@ -1862,7 +1868,7 @@ extern "C" int vggt_gemm_qkv(const void* A, int64_t lda, const void* W, int64_t 
   // (fused qkv of the 154x518 sequence chunk, 6,592 rows: 68.9 -> 53.6 us, r3w)
   if (g_vggt_gemm_tile < 0 && mode == 7 && M >= 4096 && (persist_policy(s) & 2)) mode = 9;
   if (mode == 9) {
-    bool ok = D == 64 && N % 256 == 0 && N <= PP_MAXN && K % PBK == 0 && rope_mode != VGGT_ROPE_1D &&
+    bool ok = D == 64 && nreg == 2 && N % 256 == 0 && N <= PP_MAXN && K % PBK == 0 && rope_mode != VGGT_ROPE_1D &&
               (int64_t)PBM * ldo * 2 < (1ll << 31) && ppp_lds_bytes(EPI_QKNORM_D64, ppp_pick_bm(EPI_QKNORM_D64, M, N, s), N, ep) > 0;
     if (ok && rope_mode == VGGT_ROPE_2D) {
       // positions are staged as bytes; tables of at most 256 positions
@@ -1910,4 +1916,22 @@ extern "C" int vggt_gemm_qkv(const void* A, int64_t lda, const void* W, int64_t 
   }
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
+}
+}  // namespace
+
+extern "C" int vggt_gemm_qkv(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int M, int H,
+                             int D, int K, void* out, int64_t ldo, const float* qw, const float* qb, const float* kw,
+                             const float* kb, float eps, int rope_mode, const int32_t* pos, int period,
+                             const float* cos_tab, const float* sin_tab, int tab_len, void* stream) {
+  return qkv_impl(A, lda, W, ldw, bias, M, H, D, K, out, ldo, qw, qb, kw, kb, eps, rope_mode, pos, period, cos_tab,
+                  sin_tab, tab_len, stream, 3 * H * D, 2);
+}
+
+extern "C" int vggt_gemm_headnorm(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int M,
+                                  int N, int H, int D, int K, void* out, int64_t ldo, const float* nw, const float* nb,
+                                  float eps, int rope_mode, const int32_t* pos, int period, const float* cos_tab,
+                                  const float* sin_tab, int tab_len, void* stream) {
+  if (N != H * D && N != 2 * H * D) return VGGT_ERR_SHAPE;
+  return qkv_impl(A, lda, W, ldw, bias, M, H, D, K, out, ldo, nw, nb, nullptr, nullptr, eps, rope_mode, pos, period,
+                  cos_tab, sin_tab, tab_len, stream, N, 1);
 }

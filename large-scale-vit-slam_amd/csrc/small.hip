@@ -22,6 +22,91 @@ namespace {
 // disabled: featureAligned_vggt.py:104, alignment_head.py:340).
 typedef __attribute__((ext_vector_type(4))) float f4;
 
+// One wave's share of the skinny fp32 GEMM: acc[mt] (rows 16mt + 4q + i, column
+// n0 + (lane & 15)) += act(A)[rows, kbeg:kend) . W[col, kbeg:kend)^T.  A rows past M
+// read row M-1 (never stored); columns past N read column N-1 (never stored).
+template <int ACT_IN, int MT = 4>
+__device__ __forceinline__ void wave_linear_f32(const float* __restrict__ A, int64_t lda,
+                                                const float* __restrict__ W, int64_t ldw, int M, int N, int K,
+                                                int n0, int kbeg, int kend, int lane, f32x4 (&acc)[MT]) {
+  const int r = lane & 15, q = lane >> 4;
+  const int nrow = min(n0 + r, N - 1);
+  const int mt_n = min(MT, (M + 15) / 16);
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0, 0, 0, 0};
+  const bool vec = ((K & 3) == 0) && ((lda & 3) == 0) && ((ldw & 3) == 0);
+  int k0 = kbeg;
+  if (vec) {
+    // Steady state, 64 k per iteration with no per-element guards: all of an
+    // iteration's W and A float4 loads are issued before its MFMAs (4 + 4 x mt_n
+    // loads in flight per lane instead of one round trip per 16 k -- the loop is
+    // latency-bound at skinny M).  A rows past M read row M-1: their products
+    // only reach output rows that are never stored.  The MFMA order per
+    // accumulator is the 16-k loop's, so the sums are bitwise those of the tail
+    // form below.
+    const int kv_end = kbeg + ((kend - kbeg) / 64) * 64;
+    const float* wp = W + (int64_t)nrow * ldw + 4 * q;
+    const float* ap[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) ap[mt] = A + (int64_t)min(mt * 16 + r, M - 1) * lda + 4 * q;
+    for (; k0 < kv_end; k0 += 64) {
+      f4 wv[4], av[MT][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) wv[u] = *(const f4*)(wp + k0 + 16 * u);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        if (mt < mt_n) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) av[mt][u] = *(const f4*)(ap[mt] + k0 + 16 * u);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          if (mt >= mt_n) break;
+          f4 a4 = av[mt][u];
+          if constexpr (ACT_IN == 1) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a4[j] = a4[j] / (1.f + expf(-a4[j]));
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[j], wv[u][j], acc[mt], 0, 0, 0);
+        }
+    }
+  }
+  for (; k0 < kend; k0 += 16) {
+    const int kk = k0 + 4 * q;
+    f4 wv;
+    if (vec && kk + 3 < kend) {
+      wv = *(const f4*)(W + (int64_t)nrow * ldw + kk);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wv[j] = (kk + j < kend) ? W[(int64_t)nrow * ldw + kk + j] : 0.f;
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      if (mt >= mt_n) break;
+      const int m = mt * 16 + r;
+      f4 av = f4{0, 0, 0, 0};
+      if (m < M) {
+        if (vec && kk + 3 < kend) {
+          av = *(const f4*)(A + (int64_t)m * lda + kk);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) av[j] = (kk + j < kend) ? A[(int64_t)m * lda + kk + j] : 0.f;
+        }
+        if constexpr (ACT_IN == 1) {  // SiLU on the input (poseLN_modulation = Sequential(SiLU, Linear))
+#pragma unroll
+          for (int j = 0; j < 4; ++j) av[j] = av[j] / (1.f + expf(-av[j]));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], wv[j], acc[mt], 0, 0, 0);
+    }
+  }
+}
+
 template <int ACT_IN, int EPI>
 __global__ __launch_bounds__(256) void linear_f32_kernel(const float* __restrict__ A, int64_t lda,
                                                          const float* __restrict__ W, int64_t ldw,
@@ -49,80 +134,9 @@ __global__ __launch_bounds__(256) void linear_f32_kernel(const float* __restrict
   out += (int64_t)mbase * ldo;
   M = min(M - mbase, 64);
   const int r = lane & 15, q = lane >> 4;
-  const int nrow = min(n0 + r, N - 1);
   const int mt_n = (M + 15) / 16;
-  f32x4 acc[4] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
-  const bool vec = ((K & 3) == 0) && ((lda & 3) == 0) && ((ldw & 3) == 0);
-  int k0 = kbeg;
-  if (vec) {
-    // Steady state, 64 k per iteration with no per-element guards: all of an
-    // iteration's W and A float4 loads are issued before its MFMAs (4 + 4 x mt_n
-    // loads in flight per lane instead of one round trip per 16 k -- the loop is
-    // latency-bound at skinny M).  A rows past M read row M-1: their products
-    // only reach output rows that are never stored.  The MFMA order per
-    // accumulator is the 16-k loop's, so the sums are bitwise those of the tail
-    // form below.
-    const int kv_end = kbeg + ((kend - kbeg) / 64) * 64;
-    const float* wp = W + (int64_t)nrow * ldw + 4 * q;
-    const float* ap[4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) ap[mt] = A + (int64_t)min(mt * 16 + r, M - 1) * lda + 4 * q;
-    for (; k0 < kv_end; k0 += 64) {
-      f4 wv[4], av[4][4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) wv[u] = *(const f4*)(wp + k0 + 16 * u);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        if (mt < mt_n) {
-#pragma unroll
-          for (int u = 0; u < 4; ++u) av[mt][u] = *(const f4*)(ap[mt] + k0 + 16 * u);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          if (mt >= mt_n) break;
-          f4 a4 = av[mt][u];
-          if constexpr (ACT_IN == 1) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) a4[j] = a4[j] / (1.f + expf(-a4[j]));
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[j], wv[u][j], acc[mt], 0, 0, 0);
-        }
-    }
-  }
-  for (; k0 < kend; k0 += 16) {
-    const int kk = k0 + 4 * q;
-    f4 wv;
-    if (vec && kk + 3 < kend) {
-      wv = *(const f4*)(W + (int64_t)nrow * ldw + kk);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) wv[j] = (kk + j < kend) ? W[(int64_t)nrow * ldw + kk + j] : 0.f;
-    }
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      if (mt >= mt_n) break;
-      const int m = mt * 16 + r;
-      f4 av = f4{0, 0, 0, 0};
-      if (m < M) {
-        if (vec && kk + 3 < kend) {
-          av = *(const f4*)(A + (int64_t)m * lda + kk);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) av[j] = (kk + j < kend) ? A[(int64_t)m * lda + kk + j] : 0.f;
-        }
-        if constexpr (ACT_IN == 1) {  // SiLU on the input (poseLN_modulation = Sequential(SiLU, Linear))
-#pragma unroll
-          for (int j = 0; j < 4; ++j) av[j] = av[j] / (1.f + expf(-av[j]));
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], wv[j], acc[mt], 0, 0, 0);
-    }
-  }
+  f32x4 acc[4];
+  wave_linear_f32<ACT_IN>(A, lda, W, ldw, M, N, K, n0, kbeg, kend, lane, acc);
   // C[m = 16mt + 4q + i][n = n0 + r]
   const int n = n0 + r;
   if (part) {
@@ -184,6 +198,74 @@ __global__ __launch_bounds__(256) void linear_f32_kernel(const float* __restrict
       *op = v;
     }
   }
+}
+
+// Skinny fp32 GEMM for M <= 64, split along K INSIDE the workgroup: KW waves
+// own the same 16 output columns (blockIdx.x) and consecutive k ranges of
+// kchunk (a multiple of 64); their accumulators are summed through LDS in wave
+// order by wave 0, which applies bias and the epilogue.  No partial slabs, no
+// device-scope fences or counters (vggt_linear_f32_ws picks it for the
+// decoder / camera-trunk shapes; fixed summation order: bitwise run to run).
+template <int KW, int MT, int ACT_IN, int EPI>
+__global__ __launch_bounds__(64 * KW) void linear_f32_wk_kernel(const float* __restrict__ A, int64_t lda,
+                                                                const float* __restrict__ W, int64_t ldw,
+                                                                const float* __restrict__ bias, int M, int N, int K,
+                                                                float* out, int64_t ldo,
+                                                                const float* __restrict__ gamma, int kchunk) {
+  __shared__ f32x4 red[KW - 1][MT][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * 16;
+  const int kbeg = min(K, wave * kchunk);
+  const int kend = min(K, kbeg + kchunk);
+  const int mt_n = (M + 15) / 16;
+  f32x4 acc[MT];
+  wave_linear_f32<ACT_IN, MT>(A, lda, W, ldw, M, N, K, n0, kbeg, kend, lane, acc);
+  if (wave > 0) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+      if (mt < mt_n) red[wave - 1][mt][lane] = acc[mt];
+  }
+  __syncthreads();
+  if (wave > 0) return;
+#pragma unroll
+  for (int w = 0; w < KW - 1; ++w)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+      if (mt < mt_n) acc[mt] += red[w][mt][lane];
+  const int r = lane & 15, q = lane >> 4;
+  const int n = n0 + r;
+  if (n >= N) return;
+  const float bv = bias ? bias[n] : 0.f;
+  const float g = (EPI == VGGT_EPI_RESID_F32) ? gamma[n] : 0.f;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    if (mt >= mt_n) break;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = mt * 16 + 4 * q + i;
+      if (m >= M) continue;
+      float v = acc[mt][i] + bv;
+      float* op = out + (int64_t)m * ldo + n;
+      if constexpr (EPI == VGGT_EPI_GELU_BF16) v = gelu_erf(v);
+      if constexpr (EPI == VGGT_EPI_RESID_F32) v = *op + g * v;
+      *op = v;
+    }
+  }
+}
+
+template <int KW, int MT, int ACT_IN>
+void launch_linear_wk(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, int M, int N, int K,
+                      int epi, float* out, int64_t ldo, const float* gamma, hipStream_t s) {
+  // k ranges of whole 64-k steps (the vector loop), the last wave takes the rest
+  const int kchunk = ((K + KW - 1) / KW + 63) / 64 * 64;
+  const dim3 grid((N + 15) / 16);
+  if (epi == VGGT_EPI_F32)
+    linear_f32_wk_kernel<KW, MT, ACT_IN, VGGT_EPI_F32><<<grid, 64 * KW, 0, s>>>(A, lda, W, ldw, bias, M, N, K, out, ldo, gamma, kchunk);
+  else if (epi == VGGT_EPI_GELU_BF16)
+    linear_f32_wk_kernel<KW, MT, ACT_IN, VGGT_EPI_GELU_BF16><<<grid, 64 * KW, 0, s>>>(A, lda, W, ldw, bias, M, N, K, out, ldo, gamma, kchunk);
+  else
+    linear_f32_wk_kernel<KW, MT, ACT_IN, VGGT_EPI_RESID_F32><<<grid, 64 * KW, 0, s>>>(A, lda, W, ldw, bias, M, N, K, out, ldo, gamma, kchunk);
 }
 
 // split-K combine: out = epi(sum_z part[z] + bias), fixed summation order
@@ -427,22 +509,47 @@ extern "C" int vggt_linear_f32_ws(const float* A, int64_t lda, const float* W, i
   if (epi == VGGT_EPI_RESID_F32 && !gamma) return VGGT_ERR_SHAPE;
   if ((act_in != 0 && act_in != 1) || (epi != VGGT_EPI_F32 && epi != VGGT_EPI_GELU_BF16 && epi != VGGT_EPI_RESID_F32))
     return VGGT_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  if (M <= 64 && g_vggt_linear_wk > 0) {
+    // the in-workgroup split: each wave keeps ~g_vggt_linear_wk k (2..16 waves;
+    // at most 8 with four 16-row tiles, whose register budget 16 waves would spill)
+    const int mt = M <= 16 ? 1 : 4;
+    int kw = 2;
+    while (kw < (mt == 1 ? 16 : 8) && K > kw * g_vggt_linear_wk) kw *= 2;
+#define WK(KW_, MT_)                                                                        \
+  (act_in ? launch_linear_wk<KW_, MT_, 1>(A, lda, W, ldw, bias, M, N, K, epi, out, ldo, gamma, s) \
+          : launch_linear_wk<KW_, MT_, 0>(A, lda, W, ldw, bias, M, N, K, epi, out, ldo, gamma, s))
+    if (mt == 1) {
+      if (kw == 2) WK(2, 1);
+      else if (kw == 4) WK(4, 1);
+      else if (kw == 8) WK(8, 1);
+      else WK(16, 1);
+    } else {
+      if (kw == 2) WK(2, 4);
+      else if (kw == 4) WK(4, 4);
+      else WK(8, 4);
+    }
+#undef WK
+    HIP_LAUNCH_CHECK();
+    return VGGT_OK;
+  }
   const int gy = (M + 63) / 64;
   const int blocks = ((N + 63) / 64) * gy;
-  // split K until ~2 blocks per CU are busy (skinny M: camera head, decoder)
+  // split K until one block per CU is busy or a split would keep fewer than
+  // g_vggt_linear_split_k k (skinny M: camera head, decoder)
   int splits = 1;
-  while (splits < 16 && blocks * splits * 2 <= 512 && K / (splits * 2) >= 128) splits *= 2;
+  while (splits < VGGT_LINEAR_F32_MAX_SPLITS && blocks * splits * 2 <= 512 && K / (splits * 2) >= g_vggt_linear_split_k)
+    splits *= 2;
   const int64_t mstride = (int64_t)gy * 64 * N;
   // ws = [VGGT_LINEAR_F32_WS_COUNTERS zeroed tile words][partials]
   const size_t cbytes = VGGT_LINEAR_F32_WS_COUNTERS * sizeof(unsigned);
-  if (splits > 1 && (!ws || ws_bytes < cbytes + (size_t)splits * mstride * sizeof(float))) splits = 1;
+  while (splits > 1 && (!ws || ws_bytes < cbytes + (size_t)splits * mstride * sizeof(float))) splits /= 2;
   const int kchunk = splits > 1 ? ((K + splits - 1) / splits + 15) / 16 * 16 : K;
   float* part = splits > 1 ? (float*)((char*)ws + cbytes) : nullptr;
   // one launch (last block per tile combines) while the tile words fit
   unsigned* cnt =
       (splits > 1 && blocks <= VGGT_LINEAR_F32_WS_COUNTERS && g_vggt_linear_one_launch) ? (unsigned*)ws : nullptr;
   const dim3 grid((N + 63) / 64, gy, splits);
-  hipStream_t s = (hipStream_t)stream;
 #define LAUNCH(AI, E) \
   linear_f32_kernel<AI, E><<<grid, 256, 0, s>>>(A, lda, W, ldw, bias, M, N, K, out, ldo, gamma, kchunk, part, cnt)
   if (act_in == 0) {

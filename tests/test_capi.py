@@ -54,7 +54,9 @@ def test_tune_knobs_range_and_restore():
     lib = N.lib()
     assert lib.vggt_tune(6, 5) < 0  # the retired GEMM DMA-placement knob
     for knob, good, bad in ((N.TUNE_ATTN16, (0, 1, 2), (3, -1)),
-                            (N.TUNE_ATTN_WAVES, (2, 4, 8), (3, 16))):
+                            (N.TUNE_ATTN_WAVES, (2, 4, 8), (3, 16)),
+                            (N.TUNE_LINEAR_SPLIT_K, (128, 64, 32, 16, 4096), (8, 48, 8192)),
+                            (N.TUNE_LINEAR_WK, (0, 64, 128, 4096), (32, 96, 8192, -1))):
         first = lib.vggt_tune(knob, good[0])
         assert first >= 0
         prev = good[0]

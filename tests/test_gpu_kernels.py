@@ -469,6 +469,43 @@ def _qkv_fused_check(N, tile, D, H, mode, norm, M, K):
     assert torch.equal(out[:, 2 * C:], ref[:, 2 * C:])  # v block untouched
 
 
+@pytest.mark.parametrize("tile", [-1, 0, 2, 8])
+@pytest.mark.parametrize("M,kv,norm", [(6608, False, True), (2065, True, True), (300, True, False),
+                                       (6608, True, True)])
+def test_gemm_headnorm_matches_two_pass(N, tile, M, kv, norm):
+    """vggt_gemm_headnorm (the temporal cross-attention blocks' q / packed kv
+    projection with q_norm / k_norm + 1-D RoPE in the epilogue) against the
+    two-pass path it replaces (gemm_bf16, then headnorm_rope on the first H*D
+    columns): within one bf16 ulp, the v block of a kv projection bitwise."""
+    from aligned_vggt.backbone.layers import RopeTables
+    H, D, K = 8, 128, 1024
+    C = H * D
+    Nn = 2 * C if kv else C
+    g = torch.Generator(device="cuda").manual_seed(M + kv)
+    a = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(Nn, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
+    b = torch.randn(Nn, device="cuda", generator=g).to(torch.bfloat16).float()
+    nw, nb = (torch.rand(D, device="cuda", generator=g) + 0.5 for _ in range(2))
+    if not norm:
+        nw = nb = None
+    rp = RopeTables(torch.arange(5 if kv else 16) + 3, D, 100.0, "cuda", N.ROPE_1D)
+    args = (nw, nb, 1e-6 if norm else 0.0, N.ROPE_1D, rp.pos, rp.period, rp.cos, rp.sin)
+    ref = torch.empty(M, Nn, device="cuda", dtype=torch.bfloat16)
+    N.gemm_bf16(a, w, b, ref, N.EPI_BF16)
+    N.headnorm_rope(ref, 0, H, D, *args)
+    prev = N.tune(N.TUNE_GEMM_TILE, tile)
+    try:
+        out = torch.empty_like(ref)
+        N.gemm_headnorm(a, w, b, out, H, D, *args)
+    finally:
+        N.tune(N.TUNE_GEMM_TILE, prev)
+    torch.cuda.synchronize()
+    d = (out.float() - ref.float()).abs()
+    assert (d <= ref.float().abs() * 2 ** -7 + 1e-6).all(), d.max().item()
+    if kv:
+        assert torch.equal(out[:, C:], ref[:, C:])  # v block untouched
+
+
 @pytest.mark.parametrize("tile", [0, 4, 8, 9])
 @pytest.mark.parametrize("scale", [1.0, 40.0, 1e-6])
 def test_gemm_gelu_lut_exact(N, scale, tile):

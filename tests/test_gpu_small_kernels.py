@@ -44,14 +44,16 @@ def test_linear_f32(N, M, Nn, K, epi, act):
 @pytest.mark.parametrize("M,Nn,K,epi,act", [(16, 512, 512, 3, 0), (16, 2048, 512, 1, 0), (1, 512, 2048, 2, 0),
                                              (130, 1536, 1024, 3, 0), (16, 7, 256, 3, 0), (256, 4096, 4096, 1, 0),
                                              (16, 6144, 2048, 3, 1), (16, 512, 1024, 2, 1)])
-def test_linear_f32_split_k_one_launch(N, M, Nn, K, epi, act):
+@pytest.mark.parametrize("split_k", [128, 32])
+def test_linear_f32_split_k_one_launch(N, M, Nn, K, epi, act, split_k):
     """Skinny-M split-K (vggt_linear_f32_ws): the last split block of each output
     tile combines the partials in split order in the same launch.  Bitwise
     run-to-run (fixed order) AND bitwise equal to the two-launch form (partials,
     then a reduce launch in the same split order; VGGT_TUNE_LINEAR_ONE_LAUNCH 0),
     within fp32 rounding of an fp64 reference, incl. the SiLU-on-input form
     (act_in = 1: the camera head's adaLN modulation), and the scratch's tile
-    counters are left zero for the next call."""
+    counters are left zero for the next call.  split_k: the smallest k range a
+    split keeps (VGGT_TUNE_LINEAR_SPLIT_K; 32: up to 32 splits)."""
     import torch.nn.functional as F_
     g = torch.Generator(device="cuda").manual_seed(M * Nn + K)
     a = torch.randn(M, K, device="cuda", generator=g)
@@ -60,14 +62,20 @@ def test_linear_f32_split_k_one_launch(N, M, Nn, K, epi, act):
     gam = torch.rand(Nn, device="cuda", generator=g) if epi == 2 else None
     base = torch.randn(M, Nn, device="cuda", generator=g)
     outs = []
-    for one in (1, 1, 1, 0):
-        prev = N.tune(N.TUNE_LINEAR_ONE_LAUNCH, one)
-        try:
-            out = base.clone()
-            N.linear_f32(a, w, b, out, epi, act_in=act, gamma=gam)
-        finally:
-            N.tune(N.TUNE_LINEAR_ONE_LAUNCH, prev)
-        outs.append(out)
+    prev_k = N.tune(N.TUNE_LINEAR_SPLIT_K, split_k)
+    prev_wk = N.tune(N.TUNE_LINEAR_WK, 0)  # the cross-workgroup split form
+    try:
+        for one in (1, 1, 1, 0):
+            prev = N.tune(N.TUNE_LINEAR_ONE_LAUNCH, one)
+            try:
+                out = base.clone()
+                N.linear_f32(a, w, b, out, epi, act_in=act, gamma=gam)
+            finally:
+                N.tune(N.TUNE_LINEAR_ONE_LAUNCH, prev)
+            outs.append(out)
+    finally:
+        N.tune(N.TUNE_LINEAR_SPLIT_K, prev_k)
+        N.tune(N.TUNE_LINEAR_WK, prev_wk)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
     assert torch.equal(outs[0], outs[3]), (outs[0] - outs[3]).abs().max()  # one launch == two launches, bitwise
@@ -80,6 +88,44 @@ def test_linear_f32_split_k_one_launch(N, M, Nn, K, epi, act):
     assert _rel(outs[0].double(), ref) < 2e-6, _rel(outs[0].double(), ref)
     ws = N._split_ws(a.device, 0)
     assert int(ws[:N.LINEAR_F32_WS_COUNTERS].view(torch.int32).count_nonzero()) == 0
+
+
+@pytest.mark.parametrize("wk", [64, 128, 512])
+@pytest.mark.parametrize("M,Nn,K,epi,act", [(1, 512, 512, 3, 0), (15, 2048, 512, 1, 0), (1, 512, 2048, 2, 0),
+                                             (24, 1024, 512, 3, 0), (16, 7, 1000, 3, 0), (64, 512, 4096, 1, 0),
+                                             (16, 6144, 2048, 3, 1), (40, 512, 1024, 2, 1), (17, 96, 200, 3, 0)])
+def test_linear_f32_in_workgroup_split(N, M, Nn, K, epi, act, wk):
+    """M <= 64 on the in-workgroup split-K form (VGGT_TUNE_LINEAR_WK: 2..16
+    waves on 16 columns, partials summed in LDS in wave order): bitwise run to
+    run, within fp32 rounding of an fp64 reference (ragged K and N, the SiLU
+    input, the GELU / LayerScale-residual epilogues), and close to the
+    cross-workgroup split form it replaces."""
+    import torch.nn.functional as F_
+    g = torch.Generator(device="cuda").manual_seed(M * Nn + K + wk)
+    a = torch.randn(M, K, device="cuda", generator=g)
+    w = torch.randn(Nn, K, device="cuda", generator=g) / K ** 0.5
+    b = torch.randn(Nn, device="cuda", generator=g)
+    gam = torch.rand(Nn, device="cuda", generator=g) if epi == 2 else None
+    base = torch.randn(M, Nn, device="cuda", generator=g)
+    outs = []
+    for v in (wk, wk, 0):
+        prev = N.tune(N.TUNE_LINEAR_WK, v)
+        try:
+            out = base.clone()
+            N.linear_f32(a, w, b, out, epi, act_in=act, gamma=gam)
+        finally:
+            N.tune(N.TUNE_LINEAR_WK, prev)
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    x = F_.silu(a.double()) if act else a.double()
+    ref = x @ w.double().t() + b.double()
+    if epi == 1:
+        ref = F.gelu(ref)
+    if epi == 2:
+        ref = base.double() + gam.double() * ref
+    assert _rel(outs[0].double(), ref) < 2e-6, _rel(outs[0].double(), ref)
+    assert _rel(outs[0].double(), outs[2].double()) < 2e-6
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
