@@ -67,9 +67,10 @@ const char* vggt_version(void);
                                          fixed summation order: bitwise equal; kept for A/B and tests) */
 #define VGGT_TUNE_LINEAR_SPLIT_K 7 /* vggt_linear_f32_ws split-K: split while each split keeps at least this many
                                       k (power of two, 16..4096; default 128).  Changes the fp32 summation order */
-#define VGGT_TUNE_LINEAR_WK 8 /* vggt_linear_f32_ws with M <= 64: 0 the split-K form above, else the k range
-                                 (power of two, 64..4096; default 64) each wave of an in-workgroup split keeps (2..16 waves on
-                                 16 columns, partials summed in LDS: no scratch, no counters) */
+#define VGGT_TUNE_LINEAR_WK 8 /* vggt_linear_f32_ws with M <= 256: 0 the split-K form above, else the k range
+                                 (power of two, 64..4096; default 64) each wave of an in-workgroup split keeps (2..8 waves on
+                                 16 columns x 64 rows, partials summed in LDS: no scratch, no counters; the split depends
+                                 on K only, so each row's bits do not depend on M) */
 /* (knob 6, the persistent GEMM's DMA-placement bits, is retired: its measured-best placement is the only
    one compiled; vggt_tune(6, ...) returns VGGT_ERR_UNSUPPORTED) */
 int vggt_tune(int knob, int value);

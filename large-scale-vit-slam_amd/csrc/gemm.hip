@@ -1859,6 +1859,9 @@ int qkv_impl(const void* A, int64_t lda, const void* W, int64_t ldw, const float
   // auto: the 256-wide ping-pong form on long M (fused qkv 179 vs 239 us for the
   // 128x128 form, r1s), the 128x128 form otherwise
   int mode = g_vggt_gemm_tile;
+  // vggt_gemm_headnorm only: VGGT_HEADNORM_TILE picks its form (A/B)
+  static const int hn_tile = getenv("VGGT_HEADNORM_TILE") ? atoi(getenv("VGGT_HEADNORM_TILE")) : -1;
+  if (nreg == 1 && mode < 0) mode = hn_tile;
   if (mode < 0) mode = (M >= 4096 && K % PBK == 0) ? (N % 256 == 0 ? 7 : 6) : 0;
   if (mode >= 3 && mode <= 7 && K % PBK) mode = 2;
   if (mode == 0 && K % BK) mode = 2;

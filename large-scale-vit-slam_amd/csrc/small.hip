@@ -200,8 +200,8 @@ __global__ __launch_bounds__(256) void linear_f32_kernel(const float* __restrict
   }
 }
 
-// Skinny fp32 GEMM for M <= 64, split along K INSIDE the workgroup: KW waves
-// own the same 16 output columns (blockIdx.x) and consecutive k ranges of
+// Skinny fp32 GEMM (M <= 256), split along K INSIDE the workgroup: KW waves
+// own the same 16 output columns (blockIdx.x) of a 64-row slab (blockIdx.y) and consecutive k ranges of
 // kchunk (a multiple of 64); their accumulators are summed through LDS in wave
 // order by wave 0, which applies bias and the epilogue.  No partial slabs, no
 // device-scope fences or counters (vggt_linear_f32_ws picks it for the
@@ -213,6 +213,9 @@ __global__ __launch_bounds__(64 * KW) void linear_f32_wk_kernel(const float* __r
                                                                 float* out, int64_t ldo,
                                                                 const float* __restrict__ gamma, int kchunk) {
   __shared__ f32x4 red[KW - 1][MT][64];
+  A += (int64_t)blockIdx.y * 64 * lda;
+  out += (int64_t)blockIdx.y * 64 * ldo;
+  M = min(M - (int)blockIdx.y * 64, 64);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int n0 = blockIdx.x * 16;
@@ -259,7 +262,7 @@ void launch_linear_wk(const float* A, int64_t lda, const float* W, int64_t ldw, 
                       int epi, float* out, int64_t ldo, const float* gamma, hipStream_t s) {
   // k ranges of whole 64-k steps (the vector loop), the last wave takes the rest
   const int kchunk = ((K + KW - 1) / KW + 63) / 64 * 64;
-  const dim3 grid((N + 15) / 16);
+  const dim3 grid((N + 15) / 16, (M + 63) / 64);
   if (epi == VGGT_EPI_F32)
     linear_f32_wk_kernel<KW, MT, ACT_IN, VGGT_EPI_F32><<<grid, 64 * KW, 0, s>>>(A, lda, W, ldw, bias, M, N, K, out, ldo, gamma, kchunk);
   else if (epi == VGGT_EPI_GELU_BF16)
@@ -510,20 +513,21 @@ extern "C" int vggt_linear_f32_ws(const float* A, int64_t lda, const float* W, i
   if ((act_in != 0 && act_in != 1) || (epi != VGGT_EPI_F32 && epi != VGGT_EPI_GELU_BF16 && epi != VGGT_EPI_RESID_F32))
     return VGGT_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
-  if (M <= 64 && g_vggt_linear_wk > 0) {
-    // the in-workgroup split: each wave keeps ~g_vggt_linear_wk k (2..16 waves;
-    // at most 8 with four 16-row tiles, whose register budget 16 waves would spill)
+  if (M <= 256 && g_vggt_linear_wk > 0) {
+    // the in-workgroup split: each wave keeps ~g_vggt_linear_wk k (2..8 waves).  The
+    // wave count depends on K only, so a row's result does not depend on M (a
+    // grouped encode of three chunks gives each chunk's rows the bits of its own
+    // encode); 64-row slabs along blockIdx.y
     const int mt = M <= 16 ? 1 : 4;
     int kw = 2;
-    while (kw < (mt == 1 ? 16 : 8) && K > kw * g_vggt_linear_wk) kw *= 2;
+    while (kw < 8 && K > kw * g_vggt_linear_wk) kw *= 2;
 #define WK(KW_, MT_)                                                                        \
   (act_in ? launch_linear_wk<KW_, MT_, 1>(A, lda, W, ldw, bias, M, N, K, epi, out, ldo, gamma, s) \
           : launch_linear_wk<KW_, MT_, 0>(A, lda, W, ldw, bias, M, N, K, epi, out, ldo, gamma, s))
     if (mt == 1) {
       if (kw == 2) WK(2, 1);
       else if (kw == 4) WK(4, 1);
-      else if (kw == 8) WK(8, 1);
-      else WK(16, 1);
+      else WK(8, 1);
     } else {
       if (kw == 2) WK(2, 4);
       else if (kw == 4) WK(4, 4);

@@ -93,7 +93,8 @@ def test_linear_f32_split_k_one_launch(N, M, Nn, K, epi, act, split_k):
 @pytest.mark.parametrize("wk", [64, 128, 512])
 @pytest.mark.parametrize("M,Nn,K,epi,act", [(1, 512, 512, 3, 0), (15, 2048, 512, 1, 0), (1, 512, 2048, 2, 0),
                                              (24, 1024, 512, 3, 0), (16, 7, 1000, 3, 0), (64, 512, 4096, 1, 0),
-                                             (16, 6144, 2048, 3, 1), (40, 512, 1024, 2, 1), (17, 96, 200, 3, 0)])
+                                             (16, 6144, 2048, 3, 1), (40, 512, 1024, 2, 1), (17, 96, 200, 3, 0),
+                                             (130, 1024, 2048, 2, 0)])
 def test_linear_f32_in_workgroup_split(N, M, Nn, K, epi, act, wk):
     """M <= 64 on the in-workgroup split-K form (VGGT_TUNE_LINEAR_WK: 2..16
     waves on 16 columns, partials summed in LDS in wave order): bitwise run to
@@ -126,6 +127,16 @@ def test_linear_f32_in_workgroup_split(N, M, Nn, K, epi, act, wk):
         ref = base.double() + gam.double() * ref
     assert _rel(outs[0].double(), ref) < 2e-6, _rel(outs[0].double(), ref)
     assert _rel(outs[0].double(), outs[2].double()) < 2e-6
+    # each row's bits do not depend on M: the first 16 rows alone (a chunk's
+    # camera-trunk rows) equal their rows of the batched call (a grouped encode)
+    if M > 16:
+        prev = N.tune(N.TUNE_LINEAR_WK, wk)
+        try:
+            part = base[:16].clone()
+            N.linear_f32(a[:16], w, b, part, epi, act_in=act, gamma=gam)
+        finally:
+            N.tune(N.TUNE_LINEAR_WK, prev)
+        assert torch.equal(part, outs[0][:16])
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
