@@ -36,6 +36,7 @@ sys.path.insert(0, ROOT)
 # kernel arguments in device memory (see aligned_vggt/__init__.py), set before
 # the HIP runtime initialises
 os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+os.environ.setdefault("GPU_STREAMOPS_CP_WAIT", "1")  # the encode gate's wait on the CP (aligned_vggt/__init__.py)
 import torch  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
