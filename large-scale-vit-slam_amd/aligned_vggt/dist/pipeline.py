@@ -163,11 +163,15 @@ class ChunkPipeline:
                  gate_encode: Optional[bool] = None):
         self.model = model
         # one rank: align chunk i on the side stream while the next encode group
-        # runs (the ring's schedule with the baton kept on the device);
-        # VGGT_OVERLAP_ALIGN=1 sets the default.  time_align: HIP events around
+        # runs (the ring's planned schedule with the baton kept on the device; the
+        # planner picks the ungated form there).  Default since round 5: the W = 1
+        # sequence 1,245 -> 1,194 ms (configs[3]), 1,252 -> 1,194 ms (configs[4]),
+        # 634 -> 631 ms (configs[2]) against the sequential loop, whose results it
+        # matches bitwise (profiles/r10/c3.json, tests/test_gpu_pipeline.py).
+        # VGGT_OVERLAP_ALIGN=0: the sequential loop.  time_align: HIP events around
         # every align_chunk on its stream (align_ms()).
         if overlap_align is None:
-            overlap_align = os.environ.get("VGGT_OVERLAP_ALIGN", "0") == "1"
+            overlap_align = os.environ.get("VGGT_OVERLAP_ALIGN", "1") == "1"
         self.overlap_align = overlap_align
         self.time_align = time_align
         # reserve_cus: the encodes run on a stream masked off that many CUs (spread

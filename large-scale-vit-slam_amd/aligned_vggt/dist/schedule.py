@@ -87,10 +87,10 @@ class RingCosts:
 # measured by bench.py --config 3 (`ring_model.costs`, profiles/r9); only the RELATIVE
 # costs steer the plan.  Other shapes scale by frames x group size (job_ms).
 DEFAULT_COSTS = RingCosts(
-    core={(16, 1): 29.0, (16, 2): 51.0, (16, 3): 72.0, (8, 1): 17.0},
-    dense={(16, 1): 6.5, (16, 2): 11.5, (16, 3): 16.5, (8, 1): 3.6},
-    t_align=3.45, t_align_alone=2.62, t_pause=3.9, t_align_ungated=7.7, t_pause_ungated=1.6, hop=0.25, gather=0.5,
-    source="round-4 estimates (profiles/r8/bench/final_c3.json, profiles/r7k/c3_kernels.md)")
+    core={(16, 1): 25.0, (16, 2): 47.2, (16, 3): 61.5, (8, 1): 18.0},
+    dense={(16, 1): 7.2, (16, 2): 12.5, (16, 3): 17.8, (8, 1): 5.0},
+    t_align=2.58, t_align_alone=2.34, t_pause=3.57, t_align_ungated=6.85, t_pause_ungated=1.39, hop=0.25, gather=0.5,
+    source="bench.py --config 3, round 5 (profiles/r10/c3.json: CP-side gate wait, in-workgroup split linears)")
 
 
 def load_costs() -> RingCosts:
