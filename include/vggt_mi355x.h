@@ -276,6 +276,27 @@ int vggt_linear_f32(const float* A, int64_t lda, const float* W, int64_t ldw, co
  * each output tile, in the same launch.  The scratch's first
  * VGGT_LINEAR_F32_WS_COUNTERS words are per-tile counters: zero-fill them before a
  * scratch's first use; every call leaves them zero.  ws == NULL: no split. */
+/* `groups` independent skinny fp32 linears of one shape in one launch (M <= 256):
+ * group g reads A + g*a_gstride, W + g*w_gstride, bias + g*b_gstride and writes
+ * out + g*o_gstride (element strides); epi VGGT_EPI_F32 or VGGT_EPI_GELU_BF16.
+ * Each group's values are bitwise those of its own vggt_linear_f32_ws call
+ * (the in-workgroup split form).  Replaces GatedUpdate's per-token delta MLPs
+ * (gated_update.py:51-57: one Linear pair per memory token). */
+int vggt_linear_f32_grouped(const float* A, int64_t lda, int64_t a_gstride, const float* W, int64_t ldw,
+                            int64_t w_gstride, const float* bias, int64_t b_gstride, int M, int N, int K, int groups,
+                            int act_in, int epi, float* out, int64_t ldo, int64_t o_gstride, void* stream);
+/* GatedUpdate's elementwise stages (gated_update.py:43-79, fp32; rows = B x Nt memory
+ * tokens of D features, contiguous):
+ *   prep: inp[b, i] = [update_b, |update_b| memory[b, i], |update_b| mean_j memory[b, j]]
+ *         ([B*Nt, 3D]) and g_in[:, D:2D] = |update_b| memory[b, i]  ([B*Nt, 2D]);
+ *   diff: g_in[:, 0:D] = deltas - memory;
+ *   tail: out = normalize(memory + sigmoid(logit) normalize(diff - (diff . memory) memory))
+ *         with F.normalize's max(|x|, 1e-12). */
+int vggt_gated_update_prep(const float* memory, const float* update, int B, int Nt, int D, float* inp, float* g_in,
+                           void* stream);
+int vggt_gated_update_diff(const float* memory, const float* deltas, int rows, int D, float* g_in, void* stream);
+int vggt_gated_update_tail(const float* memory, const float* deltas, const float* logit, int rows, int D, float* out,
+                           void* stream);
 #define VGGT_LINEAR_F32_WS_COUNTERS 1024
 #define VGGT_LINEAR_F32_MAX_SPLITS 32
 int vggt_linear_f32_ws(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, int M, int N, int K,

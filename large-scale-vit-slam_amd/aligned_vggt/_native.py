@@ -36,6 +36,11 @@ _SIGS = {
                       _vp, _i, _vp],
     "vggt_gemm_headnorm": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _i, _vp, _i64, _vp, _vp, _f, _i, _vp, _i, _vp,
                            _vp, _i, _vp],
+    "vggt_linear_f32_grouped": [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i, _i, _i, _i, _i, _i, _vp, _i64, _i64,
+                                _vp],
+    "vggt_gated_update_prep": [_vp, _vp, _i, _i, _i, _vp, _vp, _vp],
+    "vggt_gated_update_diff": [_vp, _vp, _i, _i, _vp, _vp],
+    "vggt_gated_update_tail": [_vp, _vp, _vp, _i, _i, _vp, _vp],
     "vggt_layernorm": [_vp, _i, _i64, _vp, _vp, _f, _i, _i, _vp, _i, _i64, _vp],
     "vggt_resid_add_layernorm": [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _f, _i, _i, _vp, _i64, _vp],
     "vggt_headnorm_rope": [_vp, _i64, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _i, _vp, _vp, _i, _vp],
@@ -440,6 +445,51 @@ def linear_f32(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], o
                                   _p(gamma), _p(ws), 0 if ws is None else ws.numel() * 4, _stream())
     _check(rc, "vggt_linear_f32_ws")
     return out
+
+
+def linear_f32_grouped(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], out: torch.Tensor,
+                       epi: int = EPI_F32) -> torch.Tensor:
+    """out[g] = epi(a[g] . w[g]^T + bias[g]) for g < G: a [G, M, K] (rows may be
+    strided), w [G, N, K], bias [G, N], out [G, M, N] fp32 (vggt_linear_f32_grouped)."""
+    _dev(a, "linear_f32_grouped")
+    G, M, K = a.shape
+    N_ = w.shape[1]
+    assert w.shape == (G, N_, K) and out.shape == (G, M, N_) and a.dtype == w.dtype == out.dtype == torch.float32
+    assert a.stride(2) == 1 and w.stride(2) == 1 and w.stride(1) == K and out.stride(2) == 1
+    assert bias is None or (bias.shape == (G, N_) and bias.stride(1) == 1)
+    rc = lib().vggt_linear_f32_grouped(_p(a), a.stride(1), a.stride(0), _p(w), w.stride(1), w.stride(0), _p(bias),
+                                       bias.stride(0) if bias is not None else 0, M, N_, K, G, 0, epi, _p(out),
+                                       out.stride(1), out.stride(0), _stream())
+    _check(rc, "vggt_linear_f32_grouped")
+    return out
+
+
+def gated_update_prep(memory: torch.Tensor, update: torch.Tensor, inp: torch.Tensor, g_in: torch.Tensor) -> None:
+    _dev(memory, "gated_update_prep")
+    B, Nt, D = memory.shape
+    assert memory.is_contiguous() and update.is_contiguous() and update.numel() == B * D
+    assert inp.is_contiguous() and inp.numel() == B * Nt * 3 * D and g_in.is_contiguous() and g_in.numel() == B * Nt * 2 * D
+    _check(lib().vggt_gated_update_prep(_p(memory), _p(update), B, Nt, D, _p(inp), _p(g_in), _stream()),
+           "vggt_gated_update_prep")
+
+
+def gated_update_diff(memory: torch.Tensor, deltas: torch.Tensor, g_in: torch.Tensor) -> None:
+    _dev(memory, "gated_update_diff")
+    D = memory.shape[-1]
+    rows = memory.numel() // D
+    assert memory.is_contiguous() and deltas.is_contiguous() and deltas.numel() == rows * D
+    assert g_in.is_contiguous() and g_in.numel() == rows * 2 * D
+    _check(lib().vggt_gated_update_diff(_p(memory), _p(deltas), rows, D, _p(g_in), _stream()), "vggt_gated_update_diff")
+
+
+def gated_update_tail(memory: torch.Tensor, deltas: torch.Tensor, logit: torch.Tensor, out: torch.Tensor) -> None:
+    _dev(memory, "gated_update_tail")
+    D = memory.shape[-1]
+    rows = memory.numel() // D
+    assert memory.is_contiguous() and deltas.is_contiguous() and logit.is_contiguous() and logit.numel() == rows
+    assert out.is_contiguous() and out.numel() == rows * D
+    _check(lib().vggt_gated_update_tail(_p(memory), _p(deltas), _p(logit), rows, D, _p(out), _stream()),
+           "vggt_gated_update_tail")
 
 
 _SPLIT_WS = {}

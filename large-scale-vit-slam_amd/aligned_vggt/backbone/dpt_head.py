@@ -212,6 +212,7 @@ def _conv(x: _Map, conv: nn.Conv2d, stride=1, pad=None, relu_in=False, relu_out=
           res1_relu=False, res2: _Map = None, pos=None, f32=True, split=None) -> _Map:
     """split: the consumer's gather form to write besides (or, f32=False, instead
     of) the f32 rows -- None, "plain" or "relu" (the consumer's relu_in)."""
+    yield_point(fine=True)
     packed = _pack_conv(conv)
     co, _, kh, kw = conv.weight.shape
     pad = conv.padding[0] if pad is None else pad
@@ -224,6 +225,7 @@ def _conv(x: _Map, conv: nn.Conv2d, stride=1, pad=None, relu_in=False, relu_out=
 
 
 def _convT(x: _Map, conv: nn.ConvTranspose2d, f32=True, split=None) -> _Map:
+    yield_point(fine=True)
     packed = _pack_conv(conv, transpose=True)
     ci, co, k, _ = conv.weight.shape
     assert conv.stride[0] == k and conv.padding[0] == 0
@@ -247,6 +249,7 @@ def _upsample(x: _Map, ho: int, wo: int, pos=None, f32=True, split=None, pos_sep
 def _conv_upsample(x: _Map, conv: nn.Conv2d, ho: int, wo: int, pos_sep, relu_out=False, f32=True, split=None) -> _Map:
     """conv3x3(resize(x) + pos) as one launch (vggt_conv2d_upsample_bf16x3): x's f32 rows
     at the source resolution, the resized map never materialised."""
+    yield_point(fine=True)
     _, b, w_hi, w_lo = _pack_conv(conv)
     co = conv.weight.shape[0]
     y, ys = _outputs(x.n * ho * wo, co, x.t.device, f32, split)

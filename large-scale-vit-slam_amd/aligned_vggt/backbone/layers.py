@@ -156,6 +156,7 @@ class Block(nn.Module):
             N.layernorm(xs, self.norm1.weight, self.norm1.bias, self.norm1.eps, xn)
         w, b = pack_linear(self.attn.qkv)
         qkv = ws.buf("blk_qkv", M, 3 * C, torch.bfloat16)
+        yield_point(fine=True)
         qn = self.attn.q_norm if isinstance(self.attn.q_norm, nn.LayerNorm) else None
         kn = self.attn.k_norm if isinstance(self.attn.k_norm, nn.LayerNorm) else None
         mode = rope.mode if (rope is not None and self.attn.rope is not None) else N.ROPE_NONE
@@ -182,6 +183,7 @@ class Block(nn.Module):
         N.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], ao, nb, H, n, n, D, rows, rows, rows, tag=tag)
         w, b = pack_linear(self.attn.proj)
         fal = _FUSED_ADD_LN if M >= _FUSED_ADD_LN_MIN_ROWS else 0
+        yield_point(fine=True)
         if (fal & 2) and C in (256, 512, 1024, 2048) and isinstance(self.norm2, nn.LayerNorm):
             # proj with a plain bf16 epilogue, then one row pass: x += ls1 * proj, xn = norm2(x)
             pj = ws.buf("blk_pj", M, C, torch.bfloat16)
@@ -196,6 +198,7 @@ class Block(nn.Module):
         yield_point()
         N.gemm_bf16(xn, w, b, hid, N.EPI_GELU_BF16)
         w, b = pack_linear(self.mlp.fc2)
+        yield_point(fine=True)
         # the row pass has kernels for C / 256 in {1, 2, 4, 8} only (norm.hip)
         if not ((fal & 1) and C in (256, 512, 1024, 2048)):
             N.gemm_bf16(hid, w, b, xs, N.EPI_RESID_F32, gamma=self._gamma(self.ls2, C, x.device), out2=out2)

@@ -13,6 +13,7 @@ workspaces.
 from __future__ import annotations
 
 import contextlib
+import os
 import threading
 from typing import Dict, Optional, Tuple
 
@@ -320,12 +321,18 @@ def gated(stream, gate: "EncodeGate"):
         _GATE.cur = prev
 
 
-def yield_point() -> None:
+# VGGT_GATE_FINE=1: also yield before the large GEMMs inside each block and before
+# every DPT convolution (shorter intervals of encode work still in flight when an
+# alignment starts)
+_GATE_FINE = os.environ.get("VGGT_GATE_FINE", "0") == "1"
+
+
+def yield_point(fine: bool = False) -> None:
     """A place in the encode (between transformer blocks, before each head)
     where a gated encode stream pauses while an alignment runs; a no-op
-    otherwise."""
+    otherwise.  ``fine`` points count only with VGGT_GATE_FINE=1."""
     cur = getattr(_GATE, "cur", None)
-    if cur is None:
+    if cur is None or (fine and not _GATE_FINE):
         return
     handle, gate = cur
     if torch.cuda.current_stream(gate.device).cuda_stream == handle:

@@ -1712,6 +1712,13 @@ int gemm_impl(const void* A, int64_t lda, const void* W, int64_t ldw, const floa
   int mode = g_vggt_gemm_tile;
   if (mode < 0)
     mode = (M >= 4096 && K % PBK == 0 && N % 256 == 0 && N >= 2048 && epi != VGGT_EPI_RESID_F32) ? 7 : 0;
+  // VGGT_GEMM_MID=1 (A/B): the 128-wide ping-pong form for the narrow (N <= 1024)
+  // LayerScale-residual / plain projections between 4,096 and 16,383 rows (the
+  // alignment head's 6,608-row proj / fc2: fc2 68.9 -> 64.0 us, gemmbench r10e)
+  static const int mid = getenv("VGGT_GEMM_MID") ? atoi(getenv("VGGT_GEMM_MID")) : 0;
+  if (g_vggt_gemm_tile < 0 && mid && mode == 0 && M >= 4096 && M < 16384 && N <= 1024 && N % 128 == 0 &&
+      K % PBK == 0 && (epi == VGGT_EPI_RESID_F32 || (mid & 2)))
+    mode = 6;
   // auto: the persistent ping-pong form where 256x256 tiles fill several
   // rounds of CUs (the 16x518^2 chunk: fc1 + GELU 217 -> 204 us, plain qkv
   // shape 159 -> 139 us, scripts/gemmbench.py r3i); it falls back to mode 7

@@ -211,10 +211,15 @@ __global__ __launch_bounds__(64 * KW) void linear_f32_wk_kernel(const float* __r
                                                                 const float* __restrict__ W, int64_t ldw,
                                                                 const float* __restrict__ bias, int M, int N, int K,
                                                                 float* out, int64_t ldo,
-                                                                const float* __restrict__ gamma, int kchunk) {
+                                                                const float* __restrict__ gamma, int kchunk,
+                                                                int64_t a_gs, int64_t w_gs, int64_t b_gs,
+                                                                int64_t o_gs) {
   __shared__ f32x4 red[KW - 1][MT][64];
-  A += (int64_t)blockIdx.y * 64 * lda;
-  out += (int64_t)blockIdx.y * 64 * ldo;
+  // blockIdx.z: a group of independent linears with the same shape (grouped form)
+  A += (int64_t)blockIdx.z * a_gs + (int64_t)blockIdx.y * 64 * lda;
+  W += (int64_t)blockIdx.z * w_gs;
+  if (bias) bias += (int64_t)blockIdx.z * b_gs;
+  out += (int64_t)blockIdx.z * o_gs + (int64_t)blockIdx.y * 64 * ldo;
   M = min(M - (int)blockIdx.y * 64, 64);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -259,16 +264,114 @@ __global__ __launch_bounds__(64 * KW) void linear_f32_wk_kernel(const float* __r
 
 template <int KW, int MT, int ACT_IN>
 void launch_linear_wk(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, int M, int N, int K,
-                      int epi, float* out, int64_t ldo, const float* gamma, hipStream_t s) {
+                      int epi, float* out, int64_t ldo, const float* gamma, hipStream_t s, int groups = 1,
+                      int64_t a_gs = 0, int64_t w_gs = 0, int64_t b_gs = 0, int64_t o_gs = 0) {
   // k ranges of whole 64-k steps (the vector loop), the last wave takes the rest
   const int kchunk = ((K + KW - 1) / KW + 63) / 64 * 64;
-  const dim3 grid((N + 15) / 16, (M + 63) / 64);
+  const dim3 grid((N + 15) / 16, (M + 63) / 64, groups);
   if (epi == VGGT_EPI_F32)
-    linear_f32_wk_kernel<KW, MT, ACT_IN, VGGT_EPI_F32><<<grid, 64 * KW, 0, s>>>(A, lda, W, ldw, bias, M, N, K, out, ldo, gamma, kchunk);
+    linear_f32_wk_kernel<KW, MT, ACT_IN, VGGT_EPI_F32><<<grid, 64 * KW, 0, s>>>(A, lda, W, ldw, bias, M, N, K, out, ldo, gamma, kchunk, a_gs, w_gs, b_gs, o_gs);
   else if (epi == VGGT_EPI_GELU_BF16)
-    linear_f32_wk_kernel<KW, MT, ACT_IN, VGGT_EPI_GELU_BF16><<<grid, 64 * KW, 0, s>>>(A, lda, W, ldw, bias, M, N, K, out, ldo, gamma, kchunk);
+    linear_f32_wk_kernel<KW, MT, ACT_IN, VGGT_EPI_GELU_BF16><<<grid, 64 * KW, 0, s>>>(A, lda, W, ldw, bias, M, N, K, out, ldo, gamma, kchunk, a_gs, w_gs, b_gs, o_gs);
   else
-    linear_f32_wk_kernel<KW, MT, ACT_IN, VGGT_EPI_RESID_F32><<<grid, 64 * KW, 0, s>>>(A, lda, W, ldw, bias, M, N, K, out, ldo, gamma, kchunk);
+    linear_f32_wk_kernel<KW, MT, ACT_IN, VGGT_EPI_RESID_F32><<<grid, 64 * KW, 0, s>>>(A, lda, W, ldw, bias, M, N, K, out, ldo, gamma, kchunk, a_gs, w_gs, b_gs, o_gs);
+}
+
+// The in-workgroup split: each wave keeps ~g_vggt_linear_wk k (2..8 waves).  The
+// wave count depends on K only, so a row's result does not depend on M (a
+// grouped encode of three chunks gives each chunk's rows the bits of its own
+// encode); 64-row slabs along blockIdx.y, groups along blockIdx.z.
+void linear_wk_dispatch(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, int M, int N,
+                        int K, int act_in, int epi, float* out, int64_t ldo, const float* gamma, hipStream_t s,
+                        int groups, int64_t a_gs, int64_t w_gs, int64_t b_gs, int64_t o_gs) {
+  const int mt = M <= 16 ? 1 : 4;
+  const int wk = g_vggt_linear_wk > 0 ? g_vggt_linear_wk : 64;
+  int kw = 2;
+  while (kw < 8 && K > kw * wk) kw *= 2;
+#define WK(KW_, MT_)                                                                                          \
+  (act_in ? launch_linear_wk<KW_, MT_, 1>(A, lda, W, ldw, bias, M, N, K, epi, out, ldo, gamma, s, groups, a_gs, \
+                                          w_gs, b_gs, o_gs)                                                     \
+          : launch_linear_wk<KW_, MT_, 0>(A, lda, W, ldw, bias, M, N, K, epi, out, ldo, gamma, s, groups, a_gs, \
+                                          w_gs, b_gs, o_gs))
+  if (mt == 1) {
+    if (kw == 2) WK(2, 1);
+    else if (kw == 4) WK(4, 1);
+    else WK(8, 1);
+  } else {
+    if (kw == 2) WK(2, 4);
+    else if (kw == 4) WK(4, 4);
+    else WK(8, 4);
+  }
+#undef WK
+}
+
+// ------------------------------------------------------------------------
+// GatedUpdate (gated_update.py:43-79) around its grouped linears: one wave per
+// (batch, memory token) row, D <= 1024 features, fp32 throughout.
+// prep: scale = |update_b|, inp[b, i] = [update_b, scale * memory[b, i], scale * mean_j memory[b, j]]
+// and the gate MLP's second input half, scale * memory[b, i], into g_in[:, D:2D].
+__global__ __launch_bounds__(64) void gated_update_prep_kernel(const float* __restrict__ memory,
+                                                               const float* __restrict__ update, int Nt, int D,
+                                                               float* __restrict__ inp, float* __restrict__ g_in) {
+  const int row = blockIdx.x, b = row / Nt, lane = threadIdx.x;
+  const float* u = update + (int64_t)b * D;
+  const float* mb = memory + (int64_t)b * Nt * D;
+  const float* mi = memory + (int64_t)row * D;
+  float ss = 0.f;
+  for (int e = lane; e < D; e += 64) ss += u[e] * u[e];
+  const float scale = sqrtf(wave_sum(ss));
+  float* o = inp + (int64_t)row * 3 * D;
+  float* g = g_in + (int64_t)row * 2 * D;
+  for (int e = lane; e < D; e += 64) {
+    float mean = 0.f;
+    for (int j = 0; j < Nt; ++j) mean += mb[(int64_t)j * D + e];
+    mean = mean / (float)Nt;
+    const float ms = mi[e] * scale;
+    o[e] = u[e];
+    o[D + e] = ms;
+    o[2 * D + e] = mean * scale;
+    g[D + e] = ms;
+  }
+}
+
+// gate input first half: diff = deltas - memory into g_in[:, 0:D]
+__global__ __launch_bounds__(64) void gated_update_diff_kernel(const float* __restrict__ memory,
+                                                               const float* __restrict__ deltas, int D,
+                                                               float* __restrict__ g_in) {
+  const int row = blockIdx.x, lane = threadIdx.x;
+  for (int e = lane; e < D; e += 64)
+    g_in[(int64_t)row * 2 * D + e] = deltas[(int64_t)row * D + e] - memory[(int64_t)row * D + e];
+}
+
+// out = normalize(memory + sigmoid(logit) * normalize(diff - (diff . memory) memory)),
+// F.normalize's max(|x|, 1e-12)
+__global__ __launch_bounds__(64) void gated_update_tail_kernel(const float* __restrict__ memory,
+                                                               const float* __restrict__ deltas,
+                                                               const float* __restrict__ logit, int D,
+                                                               float* __restrict__ out) {
+  const int row = blockIdx.x, lane = threadIdx.x;
+  const float* m = memory + (int64_t)row * D;
+  const float* dl = deltas + (int64_t)row * D;
+  float dot = 0.f;
+  for (int e = lane; e < D; e += 64) dot += (dl[e] - m[e]) * m[e];
+  dot = wave_sum(dot);
+  float nn = 0.f;
+  for (int e = lane; e < D; e += 64) {
+    const float o = (dl[e] - m[e]) - dot * m[e];
+    nn += o * o;
+  }
+  const float inv1 = 1.f / fmaxf(sqrtf(wave_sum(nn)), 1e-12f);
+  const float g = 1.f / (1.f + expf(-logit[row]));
+  float n2 = 0.f;
+  for (int e = lane; e < D; e += 64) {
+    const float v = m[e] + g * (((dl[e] - m[e]) - dot * m[e]) * inv1);
+    n2 += v * v;
+  }
+  const float inv2 = 1.f / fmaxf(sqrtf(wave_sum(n2)), 1e-12f);
+  for (int e = lane; e < D; e += 64) {
+    const float v = m[e] + g * (((dl[e] - m[e]) - dot * m[e]) * inv1);
+    out[(int64_t)row * D + e] = v * inv2;
+  }
 }
 
 // split-K combine: out = epi(sum_z part[z] + bias), fixed summation order
@@ -514,26 +617,7 @@ extern "C" int vggt_linear_f32_ws(const float* A, int64_t lda, const float* W, i
     return VGGT_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   if (M <= 256 && g_vggt_linear_wk > 0) {
-    // the in-workgroup split: each wave keeps ~g_vggt_linear_wk k (2..8 waves).  The
-    // wave count depends on K only, so a row's result does not depend on M (a
-    // grouped encode of three chunks gives each chunk's rows the bits of its own
-    // encode); 64-row slabs along blockIdx.y
-    const int mt = M <= 16 ? 1 : 4;
-    int kw = 2;
-    while (kw < 8 && K > kw * g_vggt_linear_wk) kw *= 2;
-#define WK(KW_, MT_)                                                                        \
-  (act_in ? launch_linear_wk<KW_, MT_, 1>(A, lda, W, ldw, bias, M, N, K, epi, out, ldo, gamma, s) \
-          : launch_linear_wk<KW_, MT_, 0>(A, lda, W, ldw, bias, M, N, K, epi, out, ldo, gamma, s))
-    if (mt == 1) {
-      if (kw == 2) WK(2, 1);
-      else if (kw == 4) WK(4, 1);
-      else WK(8, 1);
-    } else {
-      if (kw == 2) WK(2, 4);
-      else if (kw == 4) WK(4, 4);
-      else WK(8, 4);
-    }
-#undef WK
+    linear_wk_dispatch(A, lda, W, ldw, bias, M, N, K, act_in, epi, out, ldo, gamma, s, 1, 0, 0, 0, 0);
     HIP_LAUNCH_CHECK();
     return VGGT_OK;
   }
@@ -573,6 +657,42 @@ extern "C" int vggt_linear_f32_ws(const float* A, int64_t lda, const float* W, i
     else if (epi == VGGT_EPI_GELU_BF16) linear_f32_reduce<VGGT_EPI_GELU_BF16><<<rg, 256, 0, s>>>(part, splits, mstride, M, N, bias, out, ldo, gamma);
     else linear_f32_reduce<VGGT_EPI_RESID_F32><<<rg, 256, 0, s>>>(part, splits, mstride, M, N, bias, out, ldo, gamma);
   }
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+extern "C" int vggt_linear_f32_grouped(const float* A, int64_t lda, int64_t a_gstride, const float* W, int64_t ldw,
+                                       int64_t w_gstride, const float* bias, int64_t b_gstride, int M, int N, int K,
+                                       int groups, int act_in, int epi, float* out, int64_t ldo, int64_t o_gstride,
+                                       void* stream) {
+  if (M <= 0 || M > 256 || N <= 0 || K <= 0 || groups <= 0 || groups > 65535) return VGGT_ERR_SHAPE;
+  if ((act_in != 0 && act_in != 1) || (epi != VGGT_EPI_F32 && epi != VGGT_EPI_GELU_BF16)) return VGGT_ERR_UNSUPPORTED;
+  linear_wk_dispatch(A, lda, W, ldw, bias, M, N, K, act_in, epi, out, ldo, nullptr, (hipStream_t)stream, groups,
+                     a_gstride, w_gstride, b_gstride, o_gstride);
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+extern "C" int vggt_gated_update_prep(const float* memory, const float* update, int B, int Nt, int D, float* inp,
+                                      float* g_in, void* stream) {
+  if (B <= 0 || Nt <= 0 || D <= 0) return VGGT_ERR_SHAPE;
+  gated_update_prep_kernel<<<B * Nt, 64, 0, (hipStream_t)stream>>>(memory, update, Nt, D, inp, g_in);
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+extern "C" int vggt_gated_update_diff(const float* memory, const float* deltas, int rows, int D, float* g_in,
+                                      void* stream) {
+  if (rows <= 0 || D <= 0) return VGGT_ERR_SHAPE;
+  gated_update_diff_kernel<<<rows, 64, 0, (hipStream_t)stream>>>(memory, deltas, D, g_in);
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
+extern "C" int vggt_gated_update_tail(const float* memory, const float* deltas, const float* logit, int rows, int D,
+                                      float* out, void* stream) {
+  if (rows <= 0 || D <= 0) return VGGT_ERR_SHAPE;
+  gated_update_tail_kernel<<<rows, 64, 0, (hipStream_t)stream>>>(memory, deltas, logit, D, out);
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
 }

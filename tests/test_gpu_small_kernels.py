@@ -192,6 +192,33 @@ def test_gated_update_matches_reference_fixture(N, golden):
         torch.testing.assert_close(out.cpu(), torch.from_numpy(g["out"]), atol=2e-5, rtol=0)
 
 
+@pytest.mark.parametrize("B,Nt,D", [(1, 8, 512), (2, 8, 512), (3, 5, 96)])
+def test_gated_update_fused_matches_torch_form(N, B, Nt, D):
+    """The inference GatedUpdate (prep / grouped delta MLPs / diff / gate MLP /
+    tail kernels) against its fp32 torch form (forward_train under no_grad:
+    the reference's algebra, gated_update.py:43-79) at the decoder's shape and
+    a batch; the grouped linears equal per-token linear_f32 calls bitwise."""
+    from aligned_vggt.layers.gated_update import GatedUpdate
+    torch.manual_seed(B * Nt + D)
+    m = GatedUpdate(D, Nt).cuda()
+    mem = F.normalize(torch.randn(B, Nt, D, device="cuda"), dim=-1)
+    upd = torch.randn(B, 1, D, device="cuda") * 3
+    out = m(mem, upd)
+    with torch.no_grad():
+        ref = m.forward_train(mem, upd)
+    torch.testing.assert_close(out, ref, atol=2e-5, rtol=0)
+    # grouped == per token, bitwise
+    scale = upd.norm(dim=-1, keepdim=True)
+    inp = torch.cat([upd.expand_as(mem), mem * scale, mem.mean(1, keepdim=True).expand_as(mem) * scale], -1)
+    w1, b1, w2, b2 = m._packed()
+    hid = torch.empty(Nt, B, D, device="cuda")
+    N.linear_f32_grouped(inp.transpose(0, 1), w1, b1, hid, N.EPI_GELU_BF16)
+    for i, mlp in enumerate(m.delta_mlps):
+        h1 = torch.empty(B, D, device="cuda")
+        N.linear_f32(inp[:, i], mlp[0].weight, mlp[0].bias, h1, N.EPI_GELU_BF16)
+        assert torch.equal(h1, hid[i])
+
+
 def test_layernorm_grouped_and_cast(N):
     F_, P, C, skip = 3, 21, 1024, 5
     x = torch.randn(F_ * P, C, device="cuda")
