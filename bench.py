@@ -476,7 +476,11 @@ def bench_full(args, world, rank, dev):
                                             "parallelism": ("chunk pipeline x%d (RCCL baton ring)" % world
                                                             if args.workload == "sequence" else
                                                             "replicas x%d" % world)},
-            "recurrence": recurrence, "ring_model": ring_model}),
+            "recurrence": recurrence, "ring_model": ring_model,
+            # BASELINE.md §3 row C3 (configs[2]'s sequence through the fp32 oracle at 16 threads: 2,350 s, too
+            # long to re-time inside a bench run) as measured on a GPU-box host, labelled as such
+            "cpu_baseline": (_measured_row("C3", args.cpu_threads)
+                             if (args.config == 2 and world == 1 and not args.no_cpu_baseline) else None)}),
               flush=True)
 
 
@@ -588,12 +592,25 @@ def _ring_model(model, pipe, seq, S, ov, rec, t1_ms):
             core[(fr, g)], enc = timed(lambda: model.encode_chunk(x, dense=False))
             dense[(fr, g)], _ = timed(lambda: model.encode_dense(dict(enc)))
             del enc
+    # the two point-to-point transfers the model cannot measure on one GPU, priced from
+    # their bytes: the baton (post-head overlap tokens (ov+1) x (P+1) x 1024 fp32, memory
+    # tokens, last pose encoding) and a moved alignment's ship (the prefix rows S x (P+1)
+    # x 1024 fp32 + the camera pose encoding), at an assumed effective 100 GB/s on one
+    # xGMI link (153 GB/s peak) + 20 us per transfer
+    H_img, W_img = seq.shape[-2:]
+    P1 = (H_img // 14) * (W_img // 14) + 6
+    nm = model.alignment_head.num_memory_tokens if getattr(model, "enable_memory", False) else 0
+    baton_b = (ov + 1) * P1 * 1024 * 4 + nm * 512 * 4 + S * 9 * 4
+    ship_b = S * P1 * 1024 * 4 + S * 9 * 4
+    link = lambda b: round(b / 100e9 * 1e3 + 0.02, 3)  # noqa: E731
     costs = SC.RingCosts(core={k: round(v, 3) for k, v in core.items()},
                          dense={k: round(v, 3) for k, v in dense.items()},
                          t_align=rec["t_align_ms_under_load_median"] or 0.0,
                          t_align_alone=rec["t_align_ms_alone_median"] or 0.0, t_pause=0.0,
                          t_align_ungated=rec["t_align_ms_under_load_ungated_median"] or 0.0,
-                         source="bench.py --workload sequence on one MI355X (this line)")
+                         hop=link(baton_b), ship=link(ship_b),
+                         source="bench.py --workload sequence on one MI355X (this line); hop / ship from "
+                                "%.1f / %.1f MB at 100 GB/s + 20 us" % (baton_b / 1e6, ship_b / 1e6))
     # t_pause: what the overlapped W = 1 sequences spent beyond their plans' job time, per alignment
     n = len(lengths)
     for gated, seq_key in ((True, "sequence_ms_under_load"), (False, "sequence_ms_under_load_ungated")):
