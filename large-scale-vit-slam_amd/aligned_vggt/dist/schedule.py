@@ -89,7 +89,8 @@ class RingCosts:
 DEFAULT_COSTS = RingCosts(
     core={(16, 1): 25.0, (16, 2): 47.2, (16, 3): 61.5, (8, 1): 18.0},
     dense={(16, 1): 7.2, (16, 2): 12.5, (16, 3): 17.8, (8, 1): 5.0},
-    t_align=2.58, t_align_alone=2.34, t_pause=3.57, t_align_ungated=6.85, t_pause_ungated=1.39, hop=0.25, gather=0.5,
+    t_align=2.58, t_align_alone=2.34, t_pause=3.57, t_align_ungated=6.85, t_pause_ungated=1.39, hop=0.105, ship=0.29,
+    gather=0.5,
     source="bench.py --config 3, round 5 (profiles/r10/c3.json: CP-side gate wait, in-workgroup split linears)")
 
 

@@ -21,7 +21,7 @@ def main():
     torch.manual_seed(0)
     H, D, NK = 16, 64, 21984
     C = H * D
-    nqs = [int(x) for x in os.environ.get("NQS", "16384,20480,21984,24576,32768").split(",")]
+    nqs = [int(x) for x in os.environ.get("NQS", "16384,21984,24576").split(",")]
     reps = int(os.environ.get("REPS", "10"))
     k = (torch.randn(NK, C, device=dev) * 0.5).bfloat16()
     v = (torch.randn(NK, C, device=dev) * 0.5).bfloat16()
@@ -47,6 +47,44 @@ def main():
             res[str(nq)] = {"ms": round(ms, 4), "tflops": round(fl / ms / 1e9, 1), "workgroups": wgs,
                             "rounds_of_512": round(wgs / 512, 3)}
             print(nq, res[str(nq)], flush=True)
+    # the 21,984-row launch as two: whole rounds of 8-wave workgroups, then the tail on
+    # narrower workgroups (same rows per wave, finer per-CU balance)
+    nq = NK
+    for split in (16384, 12288):
+        for tail_w in (4, 2):
+            ts = []
+            for _ in range(2):
+                a = torch.cuda.Event(enable_timing=True)
+                b = torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(reps):
+                    N.attention(qa[:split], k, v, o[:split], 1, H, split, NK, D, split, NK, split)
+                    prev = N.tune(N.TUNE_ATTN_WAVES, tail_w)
+                    N.attention(qa[split:nq], k, v, o[split:nq], 1, H, nq - split, NK, D, nq - split, NK, nq - split)
+                    N.tune(N.TUNE_ATTN_WAVES, prev)
+                b.record()
+                b.synchronize()
+                ts.append(a.elapsed_time(b) / reps)
+            ms = min(ts)
+            key = f"py_split{split}_tail{tail_w}w"
+            res[key] = {"ms": round(ms, 4), "tflops": round(4.0 * nq * NK * D * H / ms / 1e9, 1)}
+            print(key, res[key], flush=True)
+    # the same inside the C entry point (VGGT_TUNE_ATTN_SPLIT), whole rounds found there
+    for sp in (0, 4, 2, 0, 4, 2):
+        prev = N.tune(N.TUNE_ATTN_SPLIT, sp)
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            N.attention(qa[:nq], k, v, o[:nq], 1, H, nq, NK, D, nq, NK, nq)
+        b.record()
+        b.synchronize()
+        N.tune(N.TUNE_ATTN_SPLIT, prev)
+        ms = a.elapsed_time(b) / reps
+        key = f"capi_split{sp}"
+        r = {"ms": round(ms, 4), "tflops": round(4.0 * nq * NK * D * H / ms / 1e9, 1)}
+        res.setdefault(key, []).append(r)
+        print(key, r, flush=True)
     print(json.dumps(res), flush=True)
 
 

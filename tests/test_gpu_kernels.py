@@ -326,6 +326,30 @@ def test_attention_global_shape_rows(N):
     assert _rel(o[rows], ref) < 1e-2
 
 
+@pytest.mark.parametrize("split", [4, 2])
+@pytest.mark.parametrize("batch,n", [(1, 16 * 1374), (1, 13 * 1374 + 5), (2, 16 * 1374)])
+def test_attention_round_balance_split_bitwise(N, split, batch, n):
+    """VGGT_TUNE_ATTN_SPLIT: the whole rounds of 8-wave workgroups as one launch and
+    the remaining row blocks on 4- / 2-wave workgroups -- every query row's
+    arithmetic is unchanged, so the output equals the single launch bitwise
+    (whether or not the shape triggers the split)."""
+    H, D = 16, 64
+    C = H * D
+    g = torch.Generator(device="cuda").manual_seed(n + split)
+    qkv = torch.randn(batch * n, 3 * C, device="cuda", generator=g).to(torch.bfloat16)
+    outs = []
+    for sp in (0, split):
+        prev = N.tune(N.TUNE_ATTN_SPLIT, sp)
+        try:
+            o = torch.empty(batch * n, C, device="cuda", dtype=torch.bfloat16)
+            N.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, batch, H, n, n, D, n, n, n)
+        finally:
+            N.tune(N.TUNE_ATTN_SPLIT, prev)
+        outs.append(o)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("variant", [3, 11, 19, 32, 96, 161])
 def test_attention_online_softmax_rescale(N, variant):
     """Force the running max to jump late (rule 26): one key with a huge score
