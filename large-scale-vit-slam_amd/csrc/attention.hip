@@ -915,52 +915,10 @@ __global__ __launch_bounds__(NW * 64, 16 / NW) void attn16_fwd_kernel(AttnArgs a
 
 }  // namespace
 
-static int attn_fwd_impl(const void* q, int64_t ldq, int64_t q_bstride, const void* k, int64_t ldk,
-                         int64_t k_bstride, const void* v, int64_t ldv, int64_t v_bstride, void* o, int64_t ldo,
-                         int64_t o_bstride, int batch, int heads, int nq, int nk, int D, float scale, void* stream,
-                         int waves);
-
-// Round balance of the long (8-wave, 256-row) launches: with 2 workgroups per CU
-// resident, a grid of 2.69 rounds (16 heads x 86 row blocks of the 21,984-token
-// global attention) leaves its last round on 96 CUs at two workgroups and on 160
-// at one, and the launch takes ~2.84 rounds of time.  VGGT_ATTN_SPLIT = w (4 or 2):
-// the whole rounds as one launch, the remaining row blocks as a second launch of
-// w-wave workgroups (the same 32 rows per wave, finer per-CU balance; knob 9).  Same
-// arithmetic per query row (rows are independent): bitwise equal.
 extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride, const void* k, int64_t ldk,
                                   int64_t k_bstride, const void* v, int64_t ldv, int64_t v_bstride, void* o,
                                   int64_t ldo, int64_t o_bstride, int batch, int heads, int nq, int nk, int D,
                                   float scale, void* stream) {
-  const int split_w = g_vggt_attn_split;
-  const bool eight = g_vggt_attn_waves == 8 && nq >= 4096;
-  const bool plain33 = g_vggt_attn_variant == 33;
-  if (split_w && eight && plain33 && batch > 0 && heads > 0) {
-    const int cus = vggt_stream_cu_count(stream);
-    const int64_t slots = 2 * (int64_t)(cus > 0 ? cus : 256);
-    const int64_t bh = (int64_t)batch * heads;
-    const int64_t rb = (nq + 255) / 256;
-    const int64_t whole = (rb * bh / slots) * slots;  // workgroups in whole rounds
-    const int64_t rb1 = whole / bh;                     // row blocks in the first launch
-    const int64_t rest = rb * bh - whole;
-    // only when the last round would put two workgroups on some CUs
-    if (rb1 > 0 && rb1 < rb && rest > slots / 2 && whole % bh == 0) {
-      const int r1 = (int)(rb1 * 256);
-      int rc = attn_fwd_impl(q, ldq, q_bstride, k, ldk, k_bstride, v, ldv, v_bstride, o, ldo, o_bstride, batch,
-                             heads, r1, nk, D, scale, stream, 8);
-      if (rc != VGGT_OK) return rc;
-      return attn_fwd_impl((const bf16_t*)q + (int64_t)r1 * ldq, ldq, q_bstride, k, ldk, k_bstride, v, ldv,
-                           v_bstride, (bf16_t*)o + (int64_t)r1 * ldo, ldo, o_bstride, batch, heads, nq - r1, nk, D,
-                           scale, stream, split_w == 2 ? 2 : 4);
-    }
-  }
-  return attn_fwd_impl(q, ldq, q_bstride, k, ldk, k_bstride, v, ldv, v_bstride, o, ldo, o_bstride, batch, heads, nq,
-                       nk, D, scale, stream, 0);
-}
-
-static int attn_fwd_impl(const void* q, int64_t ldq, int64_t q_bstride, const void* k, int64_t ldk,
-                         int64_t k_bstride, const void* v, int64_t ldv, int64_t v_bstride, void* o, int64_t ldo,
-                         int64_t o_bstride, int batch, int heads, int nq, int nk, int D, float scale, void* stream,
-                         int waves) {
   if (batch <= 0 || heads <= 0 || nq <= 0 || nk <= 0) return VGGT_ERR_SHAPE;
   if (D != 64 && D != 128) return VGGT_ERR_UNSUPPORTED;
   if ((ldq | ldk | ldv | ldo) % 8 || ((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) % 16)
@@ -976,8 +934,7 @@ static int attn_fwd_impl(const void* q, int64_t ldq, int64_t q_bstride, const vo
   // 2-wave workgroups (64 query rows; only the default offset-free variant 33
   // is instantiated) for grids that fill a fraction of one round of slots.
   const bool two_ok = (g_vggt_attn_variant & 32) && (g_vggt_attn_variant & 65) == 1;
-  int nw = (g_vggt_attn_waves == 8 && nq >= 4096) ? 8 : (g_vggt_attn_waves == 2 && two_ok) ? 2 : 4;
-  if (waves == 8 || waves == 4 || (waves == 2 && two_ok)) nw = waves;  // the round-balance split's launches
+  const int nw = (g_vggt_attn_waves == 8 && nq >= 4096) ? 8 : (g_vggt_attn_waves == 2 && two_ok) ? 2 : 4;
   const int nwg = ((nq + nw * 32 - 1) / (nw * 32)) * heads * batch;
   hipStream_t s = (hipStream_t)stream;
   // 16x16x32 matrix-core form: variant 161 forces it; variant 33 takes it for

@@ -1685,7 +1685,7 @@ inline int pp_auto_bn(int M, int N, bool allow192) {
 
 namespace {
 int gemm_impl(const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias, int M, int N, int K, int epi,
-              void* out, int64_t ldo, const float* gamma, float* out2, int64_t ldo2, void* stream) {
+              void* out, int64_t ldo, const float* gamma, float* out2, int64_t ldo2, void* stream, int force = -1) {
   if (M <= 0 || N <= 0 || K <= 0 || N % 128 || K % 32) return VGGT_ERR_SHAPE;
   if ((lda % 8) || (ldw % 8) || ((uintptr_t)A & 15) || ((uintptr_t)W & 15) || ((uintptr_t)bias & 15))
     return VGGT_ERR_ALIGN;
@@ -1709,7 +1709,7 @@ int gemm_impl(const void* A, int64_t lda, const void* W, int64_t ldw, const floa
   // workgroups per CU, so one's fp32 residual read-modify-write overlaps the
   // other's MFMAs) for the LayerScale+residual projections (proj 83 vs 90 us,
   // fc2 225 vs 234 us) and for small M.
-  int mode = g_vggt_gemm_tile;
+  int mode = force >= 0 ? force : g_vggt_gemm_tile;
   if (mode < 0)
     mode = (M >= 4096 && K % PBK == 0 && N % 256 == 0 && N >= 2048 && epi != VGGT_EPI_RESID_F32) ? 7 : 0;
   // VGGT_GEMM_MID=1 (A/B): the 128-wide ping-pong form for the narrow (N <= 1024)
@@ -1749,6 +1749,27 @@ int gemm_impl(const void* A, int64_t lda, const void* W, int64_t ldw, const floa
   if (mode == 9 && (N % 256 || N > PP_MAXN || K % PBK ||
                     (int64_t)PBM * (ldo > ldo2 ? ldo : ldo2) * 4 >= (1ll << 31)))
     mode = K % PBK ? 2 : epi == VGGT_EPI_RESID_F32 ? 0 : 7;  // the persistent form: N % 256 == 0, N <= 4096
+  // Round balance (knob 10): the persistent form hands tile t to workgroup t mod CUs, so
+  // 1,376 fc1 tiles (86 x 16, M = 21,984) take 6 tile-times on 256 CUs for 5.375 tiles
+  // of work.  With VGGT_GEMM_BALANCE=1 the whole rounds of row panels run persistent and
+  // the remaining rows on the 128x128 form (finer tiles, two per CU); rows are
+  // independent and both forms accumulate K in the same order: bitwise equal.
+  if (mode == 9 && force < 0 && g_vggt_gemm_balance) {
+    const int bm = epi == VGGT_EPI_RESID_F32 ? 192 : ppp_pick_bm(epi == VGGT_EPI_GELU_BF16 && out2 ? EPI_GELU_PRE : epi, M, N, s);
+    const int tpr = N / 256, cus = cu_count(s);
+    const int64_t ntiles = (int64_t)((M + bm - 1) / bm) * tpr;
+    const int64_t full = ntiles / cus, rem = ntiles % cus;
+    const int m1 = (int)((full * cus / tpr) * bm);
+    if (full >= 1 && rem > 0 && rem * 10 <= (int64_t)cus * 6 && m1 > 0 && m1 < M && K % BK == 0) {
+      int rc = gemm_impl(A, lda, W, ldw, bias, m1, N, K, epi, out, ldo, gamma, out2, ldo2, stream, 9);
+      if (rc != VGGT_OK) return rc;
+      const size_t osz = (epi == VGGT_EPI_BF16 || epi == VGGT_EPI_GELU_BF16) ? 2 : 4;
+      const size_t o2sz = epi == VGGT_EPI_GELU_BF16 ? 2 : 4;
+      return gemm_impl((const bf16_t*)A + (int64_t)m1 * lda, lda, W, ldw, bias, M - m1, N, K, epi,
+                       (char*)out + (size_t)m1 * ldo * osz, ldo, gamma,
+                       out2 ? (float*)((char*)out2 + (size_t)m1 * ldo2 * o2sz) : nullptr, ldo2, stream, 0);
+    }
+  }
   if (mode == 9) {
     int rc;
     switch (epi) {

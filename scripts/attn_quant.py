@@ -69,22 +69,6 @@ def main():
             key = f"py_split{split}_tail{tail_w}w"
             res[key] = {"ms": round(ms, 4), "tflops": round(4.0 * nq * NK * D * H / ms / 1e9, 1)}
             print(key, res[key], flush=True)
-    # the same inside the C entry point (VGGT_TUNE_ATTN_SPLIT), whole rounds found there
-    for sp in (0, 4, 2, 0, 4, 2):
-        prev = N.tune(N.TUNE_ATTN_SPLIT, sp)
-        a = torch.cuda.Event(enable_timing=True)
-        b = torch.cuda.Event(enable_timing=True)
-        a.record()
-        for _ in range(reps):
-            N.attention(qa[:nq], k, v, o[:nq], 1, H, nq, NK, D, nq, NK, nq)
-        b.record()
-        b.synchronize()
-        N.tune(N.TUNE_ATTN_SPLIT, prev)
-        ms = a.elapsed_time(b) / reps
-        key = f"capi_split{sp}"
-        r = {"ms": round(ms, 4), "tflops": round(4.0 * nq * NK * D * H / ms / 1e9, 1)}
-        res.setdefault(key, []).append(r)
-        print(key, r, flush=True)
     print(json.dumps(res), flush=True)
 
 

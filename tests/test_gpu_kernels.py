@@ -326,28 +326,43 @@ def test_attention_global_shape_rows(N):
     assert _rel(o[rows], ref) < 1e-2
 
 
-@pytest.mark.parametrize("split", [4, 2])
-@pytest.mark.parametrize("batch,n", [(1, 16 * 1374), (1, 13 * 1374 + 5), (2, 16 * 1374)])
-def test_attention_round_balance_split_bitwise(N, split, batch, n):
-    """VGGT_TUNE_ATTN_SPLIT: the whole rounds of 8-wave workgroups as one launch and
-    the remaining row blocks on 4- / 2-wave workgroups -- every query row's
-    arithmetic is unchanged, so the output equals the single launch bitwise
-    (whether or not the shape triggers the split)."""
-    H, D = 16, 64
-    C = H * D
-    g = torch.Generator(device="cuda").manual_seed(n + split)
-    qkv = torch.randn(batch * n, 3 * C, device="cuda", generator=g).to(torch.bfloat16)
+@pytest.mark.parametrize("M,Nn,K,epi", [(21984, 4096, 1024, 1), (21984, 1024, 4096, 2), (21984, 3072, 1024, 0),
+                                        (21984, 1024, 4096, 0), (19776, 4096, 1024, 1), (13500, 4096, 1024, 3)])
+def test_gemm_balance_split_bitwise(N, M, Nn, K, epi):
+    """VGGT_TUNE_GEMM_BALANCE: a persistent GEMM whose last round of tiles would be
+    under 60 % full runs as whole rounds + the remaining rows on the 128x128 form;
+    the output (and the residual mirror / the GELU pre-activation) equals the one
+    launch bitwise."""
+    g = torch.Generator(device="cuda").manual_seed(M + Nn + K + epi)
+    a = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(Nn, K, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
+    b = torch.randn(Nn, device="cuda", generator=g).to(torch.bfloat16).float()
+    gam = torch.rand(Nn, device="cuda", generator=g)
+    x0 = torch.randn(M, Nn, device="cuda", generator=g)
     outs = []
-    for sp in (0, split):
-        prev = N.tune(N.TUNE_ATTN_SPLIT, sp)
+    for bal in (0, 1):
+        prev = N.tune(N.TUNE_GEMM_BALANCE, bal)
         try:
-            o = torch.empty(batch * n, C, device="cuda", dtype=torch.bfloat16)
-            N.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, batch, H, n, n, D, n, n, n)
+            if epi == N.EPI_RESID_F32:
+                out = x0.clone()
+                o2 = torch.zeros(M, Nn, device="cuda")
+                N.gemm_bf16(a, w, b, out, epi, gamma=gam, out2=o2)
+                outs.append((out, o2))
+            elif epi == N.EPI_GELU_BF16:
+                out = torch.empty(M, Nn, device="cuda", dtype=torch.bfloat16)
+                pre = torch.empty(M, Nn, device="cuda", dtype=torch.bfloat16)
+                N.gemm_bf16(a, w, b, out, epi)
+                N.gemm_bf16_gelu_pre(a, w, b, out.clone(), pre)
+                outs.append((out, pre))
+            else:
+                out = torch.empty(M, Nn, device="cuda", dtype=torch.bfloat16 if epi == 0 else torch.float32)
+                N.gemm_bf16(a, w, b, out, epi)
+                outs.append((out,))
         finally:
-            N.tune(N.TUNE_ATTN_SPLIT, prev)
-        outs.append(o)
+            N.tune(N.TUNE_GEMM_BALANCE, prev)
     torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
+    for x, y in zip(outs[0], outs[1]):
+        assert torch.equal(x, y), (x.float() - y.float()).abs().max().item()
 
 
 @pytest.mark.parametrize("variant", [3, 11, 19, 32, 96, 161])
