@@ -70,6 +70,8 @@ class Attention(nn.Module):
 # q/k norm + RoPE fused into the qkv GEMM epilogue (vggt_gemm_qkv); VGGT_FUSED_QKV=0
 # selects the separate headnorm_rope launch (A/B and fallback for odd shapes).
 _FUSED_QKV = os.environ.get("VGGT_FUSED_QKV", "1") != "0"
+# head_dim 128 (the alignment head's frame blocks) has no persistent fused form: A/B switch
+_FUSED_QKV128 = os.environ.get("VGGT_FUSED_QKV128", "1") != "0"
 # VGGT_FUSED_ADD_LN bits: 1 = fc2 as a plain GEMM + one fused residual-add /
 # next-LayerNorm row pass (vggt_resid_add_layernorm) instead of the GEMM's fp32
 # read-modify-write epilogue + the next block's norm1; 2 = the same for proj
@@ -161,7 +163,7 @@ class Block(nn.Module):
         kn = self.attn.k_norm if isinstance(self.attn.k_norm, nn.LayerNorm) else None
         mode = rope.mode if (rope is not None and self.attn.rope is not None) else N.ROPE_NONE
         fused = _FUSED_QKV and (qn is not None) == (kn is not None) and (qn is not None or mode != N.ROPE_NONE) \
-            and D in (64, 128) and (qn is None or qn.eps == kn.eps)
+            and (D == 64 or (D == 128 and _FUSED_QKV128)) and (qn is None or qn.eps == kn.eps)
         if fused:
             # qkv projection with q_norm / k_norm + RoPE in the GEMM epilogue
             rp = rope if mode != N.ROPE_NONE else None

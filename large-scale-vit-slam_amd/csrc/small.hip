@@ -310,19 +310,23 @@ void linear_wk_dispatch(const float* A, int64_t lda, const float* W, int64_t ldw
 // (batch, memory token) row, D <= 1024 features, fp32 throughout.
 // prep: scale = |update_b|, inp[b, i] = [update_b, scale * memory[b, i], scale * mean_j memory[b, j]]
 // and the gate MLP's second input half, scale * memory[b, i], into g_in[:, D:2D].
-__global__ __launch_bounds__(64) void gated_update_prep_kernel(const float* __restrict__ memory,
-                                                               const float* __restrict__ update, int Nt, int D,
-                                                               float* __restrict__ inp, float* __restrict__ g_in) {
-  const int row = blockIdx.x, b = row / Nt, lane = threadIdx.x;
+__global__ __launch_bounds__(256) void gated_update_prep_kernel(const float* __restrict__ memory,
+                                                                const float* __restrict__ update, int Nt, int D,
+                                                                float* __restrict__ inp, float* __restrict__ g_in) {
+  __shared__ float part[4];
+  const int row = blockIdx.x, b = row / Nt, tid = threadIdx.x;
   const float* u = update + (int64_t)b * D;
   const float* mb = memory + (int64_t)b * Nt * D;
   const float* mi = memory + (int64_t)row * D;
   float ss = 0.f;
-  for (int e = lane; e < D; e += 64) ss += u[e] * u[e];
-  const float scale = sqrtf(wave_sum(ss));
+  for (int e = tid; e < D; e += 256) ss += u[e] * u[e];
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) part[tid >> 6] = ss;
+  __syncthreads();
+  const float scale = sqrtf((part[0] + part[1]) + (part[2] + part[3]));
   float* o = inp + (int64_t)row * 3 * D;
   float* g = g_in + (int64_t)row * 2 * D;
-  for (int e = lane; e < D; e += 64) {
+  for (int e = tid; e < D; e += 256) {
     float mean = 0.f;
     for (int j = 0; j < Nt; ++j) mean += mb[(int64_t)j * D + e];
     mean = mean / (float)Nt;
@@ -531,6 +535,106 @@ __global__ __launch_bounds__(256) void attn_small_wg_kernel(const T* __restrict_
 }
 
 // ------------------------------------------------------------------------
+// Small-window bf16 attention on the matrix cores (nq <= 16 queries, nk <= 16
+// keys, D % 16 == 0: the alignment head's temporal cross attention, 16 frames
+// against the 5 overlap frames, per patch token and head).  One wave per
+// (group, head), four per workgroup.  S^T = K Q^T with
+// v_mfma_f32_16x16x16_bf16 (lane l: keys 4(l>>4)..+3 of query l&15 in its
+// accumulator), the softmax over keys across the 4 lane groups (two xor
+// shuffles), then O^T = V^T P^T: the lane's own P values (rounded to bf16, as
+// the reference's bf16 SDPA does) are already the B operand, and its
+// accumulator holds 4 consecutive features of its query -- one 8-byte store per
+// 16 features.
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+// DT: D as a compile-time constant (64 / 128: every load of the wave issued before
+// its first MFMA), 0: runtime D
+template <int DT>
+__global__ __launch_bounds__(256) void attn_small_mfma_kernel(const bf16_t* __restrict__ q, int64_t ldq, int64_t qbs,
+                                                              const bf16_t* __restrict__ k, int64_t ldk, int64_t kbs,
+                                                              const bf16_t* __restrict__ v, int64_t ldv,
+                                                              bf16_t* __restrict__ o, int64_t ldo, int64_t obs,
+                                                              int pairs, int heads, int nq, int nk, int D_, float scale) {
+  const int D = DT ? DT : D_;
+  const int lane = threadIdx.x & 63;
+  const int pair = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pair >= pairs) return;
+  const int g = pair / heads, h = pair % heads;
+  const int r = lane & 15, grp = lane >> 4;
+  const bf16_t* qp = q + (int64_t)g * qbs * ldq + h * D;
+  const bf16_t* kp = k + (int64_t)g * kbs * ldk + h * D;
+  const bf16_t* vp = v + (int64_t)g * kbs * ldv + h * D;
+  // S^T[key][query]: A = K rows (key r), B = Q^T (query r); k-slice 4 grp .. +3 of each 16
+  f32x4 st = f32x4{0, 0, 0, 0};
+  const bool krow = r < nk, qrow = r < nq;
+  if constexpr (DT > 0) {
+    s16x4 ka[DT / 16], qb[DT / 16];
+#pragma unroll
+    for (int t = 0; t < DT / 16; ++t) {
+      ka[t] = krow ? *(const s16x4*)(kp + (int64_t)r * ldk + 16 * t + 4 * grp) : s16x4{0, 0, 0, 0};
+      qb[t] = qrow ? *(const s16x4*)(qp + (int64_t)r * ldq + 16 * t + 4 * grp) : s16x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int t = 0; t < DT / 16; ++t) st = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ka[t], qb[t], st, 0, 0, 0);
+  } else {
+    for (int d0 = 0; d0 < D; d0 += 16) {
+      s16x4 ka = s16x4{0, 0, 0, 0}, qb = s16x4{0, 0, 0, 0};
+      if (krow) ka = *(const s16x4*)(kp + (int64_t)r * ldk + d0 + 4 * grp);
+      if (qrow) qb = *(const s16x4*)(qp + (int64_t)r * ldq + d0 + 4 * grp);
+      st = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ka, qb, st, 0, 0, 0);
+    }
+  }
+  // softmax over the keys 4 grp + i of query r (keys >= nk masked)
+  float p[4];
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    p[i] = (4 * grp + i < nk) ? st[i] * scale : -INFINITY;
+    m = fmaxf(m, p[i]);
+  }
+  m = fmaxf(m, __shfl_xor(m, 16, 64));
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float l = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    p[i] = (4 * grp + i < nk) ? expf(p[i] - m) : 0.f;
+    l += p[i];
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  const float inv = 1.f / l;
+  s16x4 pb;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) pb[i] = (short)f2bf(p[i] * inv);
+  // V (nk x D, zero rows up to 16) into this wave's LDS slab with 8-byte loads, then
+  // O^T[feature][query] = V^T P^T: A = V^T (feature r of the tile, keys 4 grp .. +3)
+  extern __shared__ bf16_t vs_all[];
+  bf16_t* vs = vs_all + (threadIdx.x >> 6) * 16 * D;
+#pragma unroll 8
+  for (int c = lane; c < 16 * (D / 4); c += 64) {
+    const int key = c / (D / 4), d = (c % (D / 4)) * 4;
+    uint2 u = make_uint2(0u, 0u);
+    if (key < nk) u = *(const uint2*)(vp + (int64_t)key * ldv + d);
+    *(uint2*)(vs + key * D + d) = u;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slab is this wave's only: no barrier
+  bf16_t* op = o + (int64_t)g * obs * ldo + h * D;
+#pragma unroll 8
+  for (int d0 = 0; d0 < D; d0 += 16) {
+    s16x4 va;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) va[j] = (short)vs[(4 * grp + j) * D + d0 + r];
+    const f32x4 ot = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(va, pb, f32x4{0, 0, 0, 0}, 0, 0, 0);
+    // lane: query r, features d0 + 4 grp .. +3
+    if (qrow) {
+      uint2 u;
+      u.x = pack_bf2(ot[0], ot[1]);
+      u.y = pack_bf2(ot[2], ot[3]);
+      *(uint2*)(op + (int64_t)r * ldo + d0 + 4 * grp) = u;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------
 // fp32 per-head LayerNorm + RoPE (decoder / camera head run in fp32).
 template <int MODE>
 __global__ __launch_bounds__(64) void headnorm_rope_f32_kernel(float* __restrict__ buf, int64_t ld, int col_off,
@@ -676,7 +780,7 @@ extern "C" int vggt_linear_f32_grouped(const float* A, int64_t lda, int64_t a_gs
 extern "C" int vggt_gated_update_prep(const float* memory, const float* update, int B, int Nt, int D, float* inp,
                                       float* g_in, void* stream) {
   if (B <= 0 || Nt <= 0 || D <= 0) return VGGT_ERR_SHAPE;
-  gated_update_prep_kernel<<<B * Nt, 64, 0, (hipStream_t)stream>>>(memory, update, Nt, D, inp, g_in);
+  gated_update_prep_kernel<<<B * Nt, 256, 0, (hipStream_t)stream>>>(memory, update, Nt, D, inp, g_in);
   HIP_LAUNCH_CHECK();
   return VGGT_OK;
 }
@@ -718,6 +822,24 @@ extern "C" int vggt_attention_small(const void* q, int64_t ldq, int64_t q_bstrid
     attr_set = true;
   }
   hipStream_t s = (hipStream_t)stream;
+  // the matrix-core form for bf16 windows of <= 16 x 16 (VGGT_ATTN_SMALL_MFMA=0: the fp32 LDS form)
+  static const int use_mfma = getenv("VGGT_ATTN_SMALL_MFMA") ? atoi(getenv("VGGT_ATTN_SMALL_MFMA")) : 1;
+  if (use_mfma && dtype == VGGT_DTYPE_BF16 && nq <= 16 && nk <= 16 && D % 16 == 0 && D <= 256 &&
+      (ldq | ldk | ldv | ldo) % 4 == 0 && (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) & 7) == 0) {
+    const int pairs = batch * heads;
+    const int nwg = (pairs + 3) / 4;
+    const size_t lds_v = 4 * 16 * D * 2;
+#define VGGT_SMALL_MFMA(DT_)                                                                                       \
+  attn_small_mfma_kernel<DT_><<<nwg, 256, lds_v, s>>>((const bf16_t*)q, ldq, q_bstride, (const bf16_t*)k, ldk,       \
+                                                      k_bstride, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, o_bstride, \
+                                                      pairs, heads, nq, nk, D, scale)
+    if (D == 128) VGGT_SMALL_MFMA(128);
+    else if (D == 64) VGGT_SMALL_MFMA(64);
+    else VGGT_SMALL_MFMA(0);
+#undef VGGT_SMALL_MFMA
+    HIP_LAUNCH_CHECK();
+    return VGGT_OK;
+  }
   const int grid = batch * heads;
   const size_t lds_wg = ((size_t)(nq + nk) * (D + 1) + (size_t)nk * D + (size_t)nq * nk) * sizeof(float);
   static const int use_wg = getenv("VGGT_ATTN_SMALL_WG") ? atoi(getenv("VGGT_ATTN_SMALL_WG")) : 1;

@@ -141,7 +141,8 @@ def test_linear_f32_in_workgroup_split(N, M, Nn, K, epi, act, wk):
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("G,H,nq,nk,D", [(1375, 8, 16, 5, 128), (2, 8, 1, 24, 64), (1, 16, 75, 75, 128),
-                                          (3, 2, 7, 130 - 2, 32)])
+                                          (3, 2, 7, 130 - 2, 32), (413, 8, 16, 16, 128), (5, 3, 9, 11, 48),
+                                          (7, 2, 1, 1, 16)])
 def test_attention_small(N, dt, G, H, nq, nk, D):
     C = H * D
     g = torch.Generator(device="cuda").manual_seed(nq * nk)
