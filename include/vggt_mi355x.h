@@ -314,7 +314,12 @@ int vggt_linear_f32_ws(const float* A, int64_t lda, const float* W, int64_t ldw,
  * of CrossAttention (cross_attention.py:64-73) in the temporal blocks (S
  * queries x T keys per spatial token, alignment_head.py:368-390) and the
  * decoder (alignment_head.py:494-530), and the camera-head trunk attention.
+ * bf16 windows of <= 16 queries x <= 16 keys (D % 16 == 0) run on the matrix cores
+ * (fp32 scores, P rounded to bf16 for P.V, as the reference's bf16 SDPA) unless
+ * dtype carries VGGT_ATTN_SMALL_EXACT: the training forward, whose backward
+ * (vggt_attention_small_bwd) recomputes P in fp32 from the same formula.
  */
+#define VGGT_ATTN_SMALL_EXACT 0x100
 int vggt_attention_small(const void* q, int64_t ldq, int64_t q_bstride, const void* k, int64_t ldk, int64_t k_bstride,
                          const void* v, int64_t ldv, void* o, int64_t ldo, int64_t o_bstride, int dtype, int batch,
                          int heads, int nq, int nk, int D, float scale, void* stream);

@@ -527,12 +527,18 @@ def _split_ws(device, n_floats: int) -> torch.Tensor:
     return t
 
 
+ATTN_SMALL_EXACT = 0x100  # include/vggt_mi355x.h VGGT_ATTN_SMALL_EXACT
+
+
 def attention_small(q, k, v, o, batch: int, heads: int, nq: int, nk: int, D: int, q_bstride: int, k_bstride: int,
-                    o_bstride: int, scale: Optional[float] = None) -> None:
+                    o_bstride: int, scale: Optional[float] = None, exact: bool = False) -> None:
+    """exact: the fp32 LDS form for bf16 windows too (the training forward, which its
+    backward recomputes in fp32); else <= 16 x 16 bf16 windows run on the matrix cores."""
     _dev(q, "attention_small")
     sc = D ** -0.5 if scale is None else scale
     rc = lib().vggt_attention_small(_p(q), _ld(q), q_bstride, _p(k), _ld(k), k_bstride, _p(v), _ld(v), _p(o), _ld(o),
-                                    o_bstride, _dt(q), batch, heads, nq, nk, D, float(sc), _stream())
+                                    o_bstride, _dt(q) | (ATTN_SMALL_EXACT if exact else 0), batch, heads, nq, nk, D,
+                                    float(sc), _stream())
     _check(rc, "vggt_attention_small")
 
 

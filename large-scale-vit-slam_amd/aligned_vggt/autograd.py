@@ -339,7 +339,7 @@ class TemporalBlockFn(torch.autograd.Function):
                     k = dst
         v = kvpre[:, C:]
         ao = ws.buf("tb_ao", Mx, C, torch.bfloat16)
-        N.attention_small(q, k, v, ao, groups, H, nq, nk, D, nq, nk, nq)
+        N.attention_small(q, k, v, ao, groups, H, nq, nk, D, nq, nk, nq, exact=True)  # the backward's formula
         wp, bp = pack_linear(blk.attn.proj)
         br1 = ws.buf("tb_br1", Mx, C, torch.bfloat16)
         N.gemm_bf16(ao, wp, bp, br1, N.EPI_BF16)

@@ -824,7 +824,9 @@ extern "C" int vggt_attention_small(const void* q, int64_t ldq, int64_t q_bstrid
   hipStream_t s = (hipStream_t)stream;
   // the matrix-core form for bf16 windows of <= 16 x 16 (VGGT_ATTN_SMALL_MFMA=0: the fp32 LDS form)
   static const int use_mfma = getenv("VGGT_ATTN_SMALL_MFMA") ? atoi(getenv("VGGT_ATTN_SMALL_MFMA")) : 1;
-  if (use_mfma && dtype == VGGT_DTYPE_BF16 && nq <= 16 && nk <= 16 && D % 16 == 0 && D <= 256 &&
+  const bool exact = (dtype & VGGT_ATTN_SMALL_EXACT) != 0;
+  dtype &= ~VGGT_ATTN_SMALL_EXACT;
+  if (use_mfma && !exact && dtype == VGGT_DTYPE_BF16 && nq <= 16 && nk <= 16 && D % 16 == 0 && D <= 256 &&
       (ldq | ldk | ldv | ldo) % 4 == 0 && (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) & 7) == 0) {
     const int pairs = batch * heads;
     const int nwg = (pairs + 3) / 4;

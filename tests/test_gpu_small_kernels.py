@@ -143,13 +143,14 @@ def test_linear_f32_in_workgroup_split(N, M, Nn, K, epi, act, wk):
 @pytest.mark.parametrize("G,H,nq,nk,D", [(1375, 8, 16, 5, 128), (2, 8, 1, 24, 64), (1, 16, 75, 75, 128),
                                           (3, 2, 7, 130 - 2, 32), (413, 8, 16, 16, 128), (5, 3, 9, 11, 48),
                                           (7, 2, 1, 1, 16)])
-def test_attention_small(N, dt, G, H, nq, nk, D):
+@pytest.mark.parametrize("exact", [False, True])
+def test_attention_small(N, dt, G, H, nq, nk, D, exact):
     C = H * D
     g = torch.Generator(device="cuda").manual_seed(nq * nk)
     q = torch.randn(G * nq, C, device="cuda", generator=g).to(dt)
     kv = torch.randn(G * nk, 2 * C, device="cuda", generator=g).to(dt)
     o = torch.empty(G * nq, C, device="cuda", dtype=dt)
-    N.attention_small(q, kv[:, :C], kv[:, C:], o, G, H, nq, nk, D, nq, nk, nq)
+    N.attention_small(q, kv[:, :C], kv[:, C:], o, G, H, nq, nk, D, nq, nk, nq, exact=exact)
     qq = q.float().view(G, nq, H, D).transpose(1, 2)
     kk = kv[:, :C].float().view(G, nk, H, D).transpose(1, 2)
     vv = kv[:, C:].float().view(G, nk, H, D).transpose(1, 2)
