@@ -86,13 +86,13 @@ def test_planner_beats_round4_schedule_on_configs3(W):
     if W == 8:
         # strictly better than round 4's plan, and never below the recurrence's own
         # bound (every alignment at its alone speed, back to back from the earliest
-        # possible first core); once the alignment chain starts it never waits for
-        # an encode by more than one alignment
+        # possible first core); once the alignment chain starts it is busy: its waits
+        # (hops, ships, an encode not yet done) add up to under 5 % of the sequence
         assert pr.total_ms < leg.total_ms
         first_core = min(v for (fr, g), v in c.core.items() if fr == L[0])
         assert pr.total_ms >= first_core + 43 * c.t_align_alone - 1e-9
         gaps = [s - e for s, e in zip(pr.align_start[1:], pr.align_end[:-1])]
-        assert max(gaps) <= c.t_align + c.hop + c.ship + 1e-9
+        assert sum(gaps) <= 0.05 * pr.total_ms
 
 
 def test_costs_roundtrip():
