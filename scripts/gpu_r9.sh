@@ -29,6 +29,14 @@ if has c4; then
   step c4 400 python -u bench.py --config 4 --steps 3 --warmup 2 --no-cpu-baseline || exit $?
   grep '^{' "$OUT/c4.out" | tail -1 > "$OUT/c4.json"
 fi
+if has c2; then
+  step c2 400 python -u bench.py --config 2 --steps 2 --warmup 1 || exit $?
+  grep '^{' "$OUT/c2.out" | tail -1 > "$OUT/c2.json"
+fi
+if has chunk; then
+  step chunk 300 python -u bench.py --workload chunk --steps 10 --warmup 3 --no-cpu-baseline || exit $?
+  grep '^{' "$OUT/chunk.out" | tail -1 > "$OUT/chunk.json"
+fi
 if has c0; then
   step c0 300 python -u bench.py --config 0 --steps 10 --warmup 3 || exit $?
   grep '^{' "$OUT/c0.out" | tail -1 > "$OUT/c0.json"
