@@ -2,6 +2,7 @@
 routes every grow-only scratch lookup -- Workspace, the split-K and training
 reduction slabs -- to the store a captured graph owns, and restores the shared
 tables on exit (also when nested or on error).  CPU tensors only."""
+import os
 import pytest
 import torch
 
@@ -41,3 +42,21 @@ def test_workspace_buffers_grow_only():
         assert b.data_ptr() == a.data_ptr()
         c = ws.buf("x", 8, 8)
         assert c.shape == (8, 8) and c.data_ptr() != a.data_ptr()
+
+
+def test_package_sets_hip_runtime_flags_before_gpu_init():
+    """Importing aligned_vggt (before any GPU call) exports the HIP runtime flags the
+    hot path relies on, unless the caller set them: kernel arguments in device memory
+    and the encode gate's stream wait on the command processor (a polling-kernel wait
+    slowed every gated alignment by ~0.9 ms)."""
+    import subprocess
+    import sys
+    code = ("import os, sys; sys.path.insert(0, 'large-scale-vit-slam_amd'); import aligned_vggt; "
+            "print(os.environ.get('HIP_FORCE_DEV_KERNARG'), os.environ.get('GPU_STREAMOPS_CP_WAIT'))")
+    env = {k: v for k, v in os.environ.items() if k not in ("HIP_FORCE_DEV_KERNARG", "GPU_STREAMOPS_CP_WAIT")}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, check=True)
+    assert out.stdout.split() == ["1", "1"]
+    env["GPU_STREAMOPS_CP_WAIT"] = "0"  # a caller's choice is kept
+    out = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, check=True)
+    assert out.stdout.split() == ["1", "0"]
