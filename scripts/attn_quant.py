@@ -51,7 +51,7 @@ def main():
     # narrower workgroups (same rows per wave, finer per-CU balance)
     nq = NK
     for split in (16384, 12288):
-        for tail_w in (4, 2):
+        for tail_w in (4, 2, 40):  # 40: 4-wave tail on the 32x32x16 form (bitwise the 8-wave rows)
             ts = []
             for _ in range(2):
                 a = torch.cuda.Event(enable_timing=True)
@@ -59,9 +59,12 @@ def main():
                 a.record()
                 for _ in range(reps):
                     N.attention(qa[:split], k, v, o[:split], 1, H, split, NK, D, split, NK, split)
-                    prev = N.tune(N.TUNE_ATTN_WAVES, tail_w)
+                    prev = N.tune(N.TUNE_ATTN_WAVES, 4 if tail_w == 40 else tail_w)
+                    p16 = N.tune(N.TUNE_ATTN16, 0) if tail_w == 40 else None
                     N.attention(qa[split:nq], k, v, o[split:nq], 1, H, nq - split, NK, D, nq - split, NK, nq - split)
                     N.tune(N.TUNE_ATTN_WAVES, prev)
+                    if p16 is not None:
+                        N.tune(N.TUNE_ATTN16, p16)
                 b.record()
                 b.synchronize()
                 ts.append(a.elapsed_time(b) / reps)
