@@ -71,10 +71,7 @@ const char* vggt_version(void);
                                  (power of two, 64..4096; default 64) each wave of an in-workgroup split keeps (2..8 waves on
                                  16 columns x 64 rows, partials summed in LDS: no scratch, no counters; the split depends
                                  on K only, so each row's bits do not depend on M) */
-#define VGGT_TUNE_ATTN_SPLIT 9 /* vggt_attention_fwd, 8-wave launches of variant 33 whose grid would end on a
-                                  round with two workgroups on some CUs: 1 the whole rounds as one launch and the
-                                  remaining rows as a second launch of 4-wave workgroups on the same 32x32x16 form
-                                  (bitwise equal), 0 one launch */
+/* (knob 9 is unassigned: a round-balance split of the global attention measured no faster) */
 #define VGGT_TUNE_GEMM_BALANCE 10 /* vggt_gemm_bf16 on the persistent form: 1 the whole rounds of row panels
                                      persistent and the remaining rows on the 128x128 form when the last round
                                      would be under 60 % full (bitwise equal), 0 one launch */

@@ -152,7 +152,6 @@ TUNE_LINEAR_ONE_LAUNCH = 6
 TUNE_LINEAR_SPLIT_K = 7
 TUNE_LINEAR_WK = 8
 TUNE_GEMM_BALANCE = 10
-TUNE_ATTN_SPLIT = 9
 
 
 def tune(knob: int, value: int) -> int:

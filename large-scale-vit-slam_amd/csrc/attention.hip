@@ -915,50 +915,10 @@ __global__ __launch_bounds__(NW * 64, 16 / NW) void attn16_fwd_kernel(AttnArgs a
 
 }  // namespace
 
-static int attn_fwd_impl(const void* q, int64_t ldq, int64_t q_bstride, const void* k, int64_t ldk,
-                         int64_t k_bstride, const void* v, int64_t ldv, int64_t v_bstride, void* o, int64_t ldo,
-                         int64_t o_bstride, int batch, int heads, int nq, int nk, int D, float scale, void* stream,
-                         int waves, bool no16);
-
-// Round balance of the long 8-wave launches (knob 9, VGGT_ATTN_SPLIT): two workgroups
-// are resident per CU, so the 21,984-token global attention's 1,376 workgroups are
-// 2.69 rounds and the last one runs two workgroups on 96 CUs and one on 160
-// (profiles/r10/attn_quant_*: 1,117 TF/s against 1,185 at a whole number of
-// rounds).  Split: the whole rounds' row blocks as one launch, the remaining rows as
-// a second launch of 4-wave workgroups on the same 32x32x16 form -- rows are
-// independent and every row's arithmetic is the same: bitwise equal.
 extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride, const void* k, int64_t ldk,
                                   int64_t k_bstride, const void* v, int64_t ldv, int64_t v_bstride, void* o,
                                   int64_t ldo, int64_t o_bstride, int batch, int heads, int nq, int nk, int D,
                                   float scale, void* stream) {
-  if (g_vggt_attn_split && g_vggt_attn_variant == 33 && g_vggt_attn_waves == 8 && nq >= 4096 && batch > 0 &&
-      heads > 0 && (D == 64 || D == 128)) {
-    int cus = vggt_stream_cu_count(stream);
-    if (cus <= 0) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev))
-        cus = 256;
-    }
-    const int64_t slots = 2 * (int64_t)cus, bh = (int64_t)batch * heads, rb = (nq + 255) / 256;
-    const int64_t whole = (rb * bh / slots) * slots, rest = rb * bh - whole;
-    if (whole > 0 && whole % bh == 0 && rest > slots / 2) {  // the last round would put 2 on some CUs
-      const int r1 = (int)(whole / bh * 256);
-      int rc = attn_fwd_impl(q, ldq, q_bstride, k, ldk, k_bstride, v, ldv, v_bstride, o, ldo, o_bstride, batch,
-                             heads, r1, nk, D, scale, stream, 8, false);
-      if (rc != VGGT_OK) return rc;
-      return attn_fwd_impl((const bf16_t*)q + (int64_t)r1 * ldq, ldq, q_bstride, k, ldk, k_bstride, v, ldv,
-                           v_bstride, (bf16_t*)o + (int64_t)r1 * ldo, ldo, o_bstride, batch, heads, nq - r1, nk, D,
-                           scale, stream, 4, true);
-    }
-  }
-  return attn_fwd_impl(q, ldq, q_bstride, k, ldk, k_bstride, v, ldv, v_bstride, o, ldo, o_bstride, batch, heads, nq,
-                       nk, D, scale, stream, 0, false);
-}
-
-static int attn_fwd_impl(const void* q, int64_t ldq, int64_t q_bstride, const void* k, int64_t ldk,
-                         int64_t k_bstride, const void* v, int64_t ldv, int64_t v_bstride, void* o, int64_t ldo,
-                         int64_t o_bstride, int batch, int heads, int nq, int nk, int D, float scale, void* stream,
-                         int waves, bool no16) {
   if (batch <= 0 || heads <= 0 || nq <= 0 || nk <= 0) return VGGT_ERR_SHAPE;
   if (D != 64 && D != 128) return VGGT_ERR_UNSUPPORTED;
   if ((ldq | ldk | ldv | ldo) % 8 || ((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) % 16)
@@ -974,8 +934,7 @@ static int attn_fwd_impl(const void* q, int64_t ldq, int64_t q_bstride, const vo
   // 2-wave workgroups (64 query rows; only the default offset-free variant 33
   // is instantiated) for grids that fill a fraction of one round of slots.
   const bool two_ok = (g_vggt_attn_variant & 32) && (g_vggt_attn_variant & 65) == 1;
-  int nw = (g_vggt_attn_waves == 8 && nq >= 4096) ? 8 : (g_vggt_attn_waves == 2 && two_ok) ? 2 : 4;
-  if (waves == 8 || waves == 4) nw = waves;  // the round-balance split's launches
+  const int nw = (g_vggt_attn_waves == 8 && nq >= 4096) ? 8 : (g_vggt_attn_waves == 2 && two_ok) ? 2 : 4;
   const int nwg = ((nq + nw * 32 - 1) / (nw * 32)) * heads * batch;
   hipStream_t s = (hipStream_t)stream;
   // 16x16x32 matrix-core form: variant 161 forces it; variant 33 takes it for
@@ -986,7 +945,7 @@ static int attn_fwd_impl(const void* q, int64_t ldq, int64_t q_bstride, const vo
   // VGGT_ATTN16=2: the 16x16 form only for the 4-wave (nq < 4096: frame / DINOv2) launches
   // (never with an lse: the training recompute, vggt_attention_fwd_lse, always
   // takes the exact-score 32x32 form whose lse the backward recomputes bit for bit)
-  const bool use16 = !no16 && a.lse == nullptr && D == 64 && nw != 2 &&
+  const bool use16 = a.lse == nullptr && D == 64 && nw != 2 &&
                      (g_vggt_attn_variant == 161 ||
                       (g_vggt_attn_variant == 33 && (g_vggt_attn16 == 1 || (g_vggt_attn16 == 2 && nw == 4))));
   if (use16) {

@@ -27,8 +27,7 @@ int g_vggt_conv_pf2 = env_or("VGGT_CONV_PF2", 1);
 int g_vggt_linear_one_launch = env_or("VGGT_LINEAR_ONE_LAUNCH", 1);
 int g_vggt_linear_split_k = env_or("VGGT_LINEAR_SPLIT_K", 128);
 int g_vggt_linear_wk = env_or("VGGT_LINEAR_WK", 64);
-int g_vggt_gemm_balance = env_or("VGGT_GEMM_BALANCE", 0);
-int g_vggt_attn_split = env_or("VGGT_ATTN_SPLIT", 0);  // align_chunk 2.87 -> 2.58 ms (profiles/r10/align_*)
+int g_vggt_gemm_balance = env_or("VGGT_GEMM_BALANCE", 0);  // align_chunk 2.87 -> 2.58 ms (profiles/r10/align_*)
 
 extern "C" int vggt_tune(int knob, int value) {
   int prev;
@@ -75,11 +74,6 @@ extern "C" int vggt_tune(int knob, int value) {
       if (value != 0 && (value < 64 || value > 4096 || (value & (value - 1)))) return VGGT_ERR_UNSUPPORTED;
       prev = g_vggt_linear_wk;
       g_vggt_linear_wk = value;
-      return prev;
-    case VGGT_TUNE_ATTN_SPLIT:
-      if (value != 0 && value != 1) return VGGT_ERR_UNSUPPORTED;
-      prev = g_vggt_attn_split;
-      g_vggt_attn_split = value;
       return prev;
     case VGGT_TUNE_GEMM_BALANCE:
       if (value != 0 && value != 1) return VGGT_ERR_UNSUPPORTED;

@@ -720,12 +720,7 @@ extern "C" int vggt_linear_f32_ws(const float* A, int64_t lda, const float* W, i
   if ((act_in != 0 && act_in != 1) || (epi != VGGT_EPI_F32 && epi != VGGT_EPI_GELU_BF16 && epi != VGGT_EPI_RESID_F32))
     return VGGT_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
-  // the in-workgroup split for K <= VGGT_LINEAR_WK_MAXK (2048: the decoder, GatedUpdate and the camera
-  // trunk's K = 2048 projections); beyond it (the camera trunk's fc2, K = 8192, N = 2048: 128 workgroups
-  // of 16 columns would leave half the CUs idle) the cross-workgroup split below -- a choice by K only,
-  // so a row's bits still do not depend on M
-  static const int wk_maxk = getenv("VGGT_LINEAR_WK_MAXK") ? atoi(getenv("VGGT_LINEAR_WK_MAXK")) : 2048;
-  if (M <= 256 && g_vggt_linear_wk > 0 && K <= wk_maxk) {
+  if (M <= 256 && g_vggt_linear_wk > 0) {
     linear_wk_dispatch(A, lda, W, ldw, bias, M, N, K, act_in, epi, out, ldo, gamma, s, 1, 0, 0, 0, 0);
     HIP_LAUNCH_CHECK();
     return VGGT_OK;

@@ -8,7 +8,6 @@ extern int g_vggt_conv_pf2;     // split-bf16 conv: 1 two-deep buffer-load gathe
 extern int g_vggt_linear_split_k;    // split-K vggt_linear_f32_ws: split while each split keeps >= this many k (2 splits' worth)
 extern int g_vggt_linear_one_launch; // split-K vggt_linear_f32_ws: 1 combine in the same launch (default), 0 reduce launch
 extern int g_vggt_linear_wk;         // vggt_linear_f32_ws, M <= 256: in-workgroup split-K, ~this many k per wave (0: off)
-extern int g_vggt_attn_split;         // 1: long 8-wave attention launches split for round balance (whole rounds + 4-wave tail)
 extern int g_vggt_gemm_balance;      // 1: persistent GEMMs with a partial last round split (whole rounds persistent, rest 128x128)
 // per-stream launch configuration (vggt_set_stream_config): the CUs a CU-masked
 // stream may use (0: the device's) and its VGGT_STREAM_* flags

@@ -72,22 +72,6 @@ def main():
             key = f"py_split{split}_tail{tail_w}w"
             res[key] = {"ms": round(ms, 4), "tflops": round(4.0 * nq * NK * D * H / ms / 1e9, 1)}
             print(key, res[key], flush=True)
-    # the same split inside vggt_attention_fwd (VGGT_TUNE_ATTN_SPLIT), alternated
-    for _ in range(2):
-        for sp in (0, 1):
-            prev = N.tune(N.TUNE_ATTN_SPLIT, sp)
-            a = torch.cuda.Event(enable_timing=True)
-            b = torch.cuda.Event(enable_timing=True)
-            a.record()
-            for _ in range(reps):
-                N.attention(qa[:nq], k, v, o[:nq], 1, H, nq, NK, D, nq, NK, nq)
-            b.record()
-            b.synchronize()
-            N.tune(N.TUNE_ATTN_SPLIT, prev)
-            ms = a.elapsed_time(b) / reps
-            r = {"ms": round(ms, 4), "tflops": round(4.0 * nq * NK * D * H / ms / 1e9, 1)}
-            res.setdefault(f"capi_split{sp}", []).append(r)
-            print(f"capi_split{sp}", r, flush=True)
     print(json.dumps(res), flush=True)
 
 

@@ -57,8 +57,7 @@ def test_tune_knobs_range_and_restore():
                             (N.TUNE_ATTN_WAVES, (2, 4, 8), (3, 16)),
                             (N.TUNE_LINEAR_SPLIT_K, (128, 64, 32, 16, 4096), (8, 48, 8192)),
                             (N.TUNE_LINEAR_WK, (0, 64, 128, 4096), (32, 96, 8192, -1)),
-                            (N.TUNE_GEMM_BALANCE, (0, 1), (2, -1)),
-                            (N.TUNE_ATTN_SPLIT, (0, 1), (2, -1))):
+                            (N.TUNE_GEMM_BALANCE, (0, 1), (2, -1))):
         first = lib.vggt_tune(knob, good[0])
         assert first >= 0
         prev = good[0]

@@ -326,29 +326,6 @@ def test_attention_global_shape_rows(N):
     assert _rel(o[rows], ref) < 1e-2
 
 
-@pytest.mark.parametrize("batch,n,D,H", [(1, 16 * 1374, 64, 16), (1, 13 * 1374 + 5, 64, 16), (2, 16 * 1374, 64, 16),
-                                         (1, 21000, 128, 8), (1, 4100, 64, 16)])
-def test_attention_round_balance_split_bitwise(N, batch, n, D, H):
-    """VGGT_TUNE_ATTN_SPLIT: the whole rounds of 8-wave workgroups as one launch and the
-    remaining rows as a second launch of 4-wave workgroups on the same 32x32x16 form:
-    every query row's arithmetic is unchanged, so the output equals the single launch
-    bitwise (whether or not the shape triggers the split)."""
-    C = H * D
-    g = torch.Generator(device="cuda").manual_seed(n + D)
-    qkv = torch.randn(batch * n, 3 * C, device="cuda", generator=g).to(torch.bfloat16)
-    outs = []
-    for sp in (0, 1):
-        prev = N.tune(N.TUNE_ATTN_SPLIT, sp)
-        try:
-            o = torch.full((batch * n, C), float("nan"), device="cuda", dtype=torch.bfloat16)
-            N.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, batch, H, n, n, D, n, n, n)
-        finally:
-            N.tune(N.TUNE_ATTN_SPLIT, prev)
-        outs.append(o)
-    torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
-
-
 @pytest.mark.parametrize("M,Nn,K,epi", [(21984, 4096, 1024, 1), (21984, 1024, 4096, 2), (21984, 3072, 1024, 0),
                                         (21984, 1024, 4096, 0), (19776, 4096, 1024, 1), (13500, 4096, 1024, 3)])
 def test_gemm_balance_split_bitwise(N, M, Nn, K, epi):
