@@ -329,13 +329,34 @@ def plan_ring(lengths: Sequence[int], W: int, costs: Optional[RingCosts] = None,
     plans = build(choice)
     if offload and W > 1:
         plans, pr = _offload(lengths, W, plans, costs, pr)
+        # one more pass over each rank's plan with the alignments where the moves put
+        # them (a rank relieved of its alignments may now prefer other groups), then
+        # the moves again from there
+        key = lambda p: (round(p.total_ms, 6), round(max(p.rank_finish), 6), round(sum(p.rank_finish), 6))  # noqa: E731
+        ar = list(plans[0].align_rank)
+        changed = False
+        for r in range(W):
+            for opt in options[r]:
+                if opt == choice[r]:
+                    continue
+                trial = list(choice)
+                trial[r] = opt
+                tp = build(trial)
+                for pl in tp:
+                    pl.align_rank = tuple(ar)
+                p2 = simulate(lengths, W, tp, costs)
+                if key(p2) < key(pr):
+                    choice, plans, pr, changed = trial, tp, p2, True
+        if changed:
+            plans, pr = _offload(lengths, W, plans, costs, pr, ar)
     return plans, pr
 
 
-def _offload(lengths, W, plans, costs, pr):
-    """Greedy alignment moves off the last-finishing rank (see plan_ring)."""
+def _offload(lengths, W, plans, costs, pr, ar0=None):
+    """Greedy alignment moves off the last-finishing rank (see plan_ring), from
+    the owners (or from ``ar0``)."""
     n = len(lengths)
-    ar = list(i % W for i in range(n))
+    ar = list(ar0) if ar0 is not None else list(i % W for i in range(n))
 
     def with_ar(a):
         for pl in plans:
