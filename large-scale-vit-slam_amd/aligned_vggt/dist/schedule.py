@@ -267,7 +267,7 @@ _POLICIES = ("with", "lag", "end")
 
 def plan_ring(lengths: Sequence[int], W: int, costs: Optional[RingCosts] = None, cap: int = 3,
               policies: Sequence[str] = _POLICIES, gates: Sequence[bool] = (True, False),
-              sweeps: int = 2, offload: bool = True) -> Tuple[List[RankPlan], Prediction]:
+              sweeps: int = 2, offload: bool = True, refine: bool = True) -> Tuple[List[RankPlan], Prediction]:
     """Per-rank plans minimising the predicted sequence time: each rank's
     longest equal-length run is cut into groups of <= cap chunks (every
     composition tried) under each DPT placement policy, gated or not, rank by rank, a few
@@ -275,8 +275,9 @@ def plan_ring(lengths: Sequence[int], W: int, costs: Optional[RingCosts] = None,
     alignments move, one at a time, from the rank that finishes last to the
     ranks that finish first while the prediction improves: 43 chunks over 8
     ranks leave two ranks six chunks, and their alignments' gate pauses are
-    what keeps them last.  Deterministic, so every rank computes the same
-    plans."""
+    what keeps them last.  With ``refine``, one more pass over each rank's
+    options with the alignments fixed where they went, then the moves again.
+    Deterministic, so every rank computes the same plans."""
     costs = costs or load_costs()
     n = len(lengths)
     owns = [list(range(r, n, W)) for r in range(W)]
@@ -329,6 +330,7 @@ def plan_ring(lengths: Sequence[int], W: int, costs: Optional[RingCosts] = None,
     plans = build(choice)
     if offload and W > 1:
         plans, pr = _offload(lengths, W, plans, costs, pr)
+    if offload and W > 1 and refine:
         # one more pass over each rank's plan with the alignments where the moves put
         # them (a rank relieved of its alignments may now prefer other groups), then
         # the moves again from there

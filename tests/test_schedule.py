@@ -99,3 +99,19 @@ def test_costs_roundtrip():
     c = SC.DEFAULT_COSTS
     d = c.to_json()
     assert SC.RingCosts.from_json(d) == c
+
+
+@pytest.mark.parametrize("W", [2, 4])
+def test_refine_never_worse_and_keeps_ownership(W):
+    """The re-plan pass after the alignment moves only accepts a better
+    prediction, and its alignments still sit on valid ranks with the same
+    assignment on every rank's plan (configs[3]/[4] chunking)."""
+    L = [len(c) for c in generate_chunks(512, "chunk_overlap", 16, 4)]
+    c = SC.DEFAULT_COSTS
+    _, base = SC.plan_ring(L, W, c, refine=False)
+    plans, pr = SC.plan_ring(L, W, c)
+    assert pr.total_ms <= base.total_ms + 1e-9
+    ar = plans[0].align_rank
+    assert len(ar) == len(L) and all(0 <= a < W for a in ar)
+    assert all(pl.align_rank == ar for pl in plans)
+    assert SC.simulate(L, W, plans, c).total_ms == pytest.approx(pr.total_ms)
