@@ -217,7 +217,16 @@ class ChunkPipeline:
         # rank's encode is gated; these restrict its choices
         self.plan_policies = tuple(os.environ.get("VGGT_RING_POLICIES", "with,lag,end").split(","))
         self.plan_gates = (True, False)
-        self.plan_offload = os.environ.get("VGGT_RING_OFFLOAD", "1") != "0"
+        # alignments moved off their owner ride a second process group (ships) between
+        # the same rank pairs as the batons; the model credits them only 1.7-3 % at
+        # W = 8, priced at an assumed link speed, and their progress
+        # relies on RCCL's p2p kernels co-residing with the persistent encode kernels.
+        # Off by default until a measured 8-GPU run shows it pays: VGGT_RING_OFFLOAD=1.
+        self.plan_offload = os.environ.get("VGGT_RING_OFFLOAD", "0") == "1"
+        # device-memory bound on the ring's plans: the core results a rank holds for a
+        # later DPT job ("end" / "lag" policies) stay under this many bytes
+        # (dist/schedule.py plan_ring max_held); VGGT_RING_HELD_GB
+        self.held_budget = float(os.environ.get("VGGT_RING_HELD_GB", "24")) * (1 << 30)
         self._local = None
         self.prediction = None
 
@@ -322,7 +331,10 @@ class ChunkPipeline:
         done = self.__dict__.setdefault("_p2p_done", set())
         if ship_pairs and self.__dict__.get("_ship_group") is None:
             ranks = dist.get_process_group_ranks(self.group) if self.group is not None else list(range(W))
-            self._ship_group = dist.new_group(ranks=ranks, backend=dist.get_backend(self.group))
+            # local synchronisation: only the ring's own ranks make this call (the ring may
+            # run on a subgroup of a larger job, whose other ranks never get here)
+            self._ship_group = dist.new_group(ranks=ranks, backend=dist.get_backend(self.group),
+                                              use_local_synchronization=True)
         for pairs, grp in ((key[0], self.group), (key[1], self.__dict__.get("_ship_group"))):
             if not pairs or (pairs, id(grp)) in done:
                 continue
@@ -403,6 +415,20 @@ class ChunkPipeline:
         n = max(len(c) for c in chunks)
         return max(1, min(self.encode_group, GROUP_TOKENS // (B * n * P)))
 
+    def _held_chunk_bytes(self, chunks, images) -> int:
+        """Device bytes one chunk's core result keeps while it waits for its DPT
+        job: the kept aggregator layers (S, P, 2C) fp32, the alignment head's
+        prefix rows (S, P + 1, C) fp32 and the frames."""
+        B, H, W = images.shape[0], images.shape[-2], images.shape[-1]
+        agg = getattr(self.model, "aggregator", None)
+        ps = getattr(agg, "patch_size", 14)
+        ps = ps[0] if isinstance(ps, (tuple, list)) else int(ps)
+        P = (H // ps) * (W // ps) + int(getattr(agg, "patch_start_idx", 5))
+        C = int(getattr(self.model, "embed_dim", 1024))
+        S = max(len(c) for c in chunks)
+        n_layers = len(getattr(self.model, "intermediate_layer_indices", (4, 11, 17, 23)))
+        return 4 * B * S * (n_layers * P * 2 * C + (P + 1) * C + 3 * H * W)
+
     def plans(self, chunks, images, cuda: bool):
         """This ring's per-rank encode plans (dist/schedule.py ``plan_ring``:
         group sizes, where the DPT heads run, gated or not; cached per
@@ -421,7 +447,8 @@ class ChunkPipeline:
         # no-grad inference with VGGT_ALIGN_PREFIX on)
         offload = self.plan_offload and W > 1 and hasattr(self.model, "ship_spec") and \
             self.model.ship_spec(images.shape[0], lengths[0], *images.shape[-2:]) is not None
-        key = (tuple(lengths), W, cap, policies, gates, legacy, offload)
+        max_held = max(cap, int(self.held_budget // max(1, self._held_chunk_bytes(chunks, images))))
+        key = (tuple(lengths), W, cap, policies, gates, legacy, offload, max_held)
         cache = self.__dict__.setdefault("_plan_cache", {})
         if key not in cache:
             costs = SC.load_costs()
@@ -431,7 +458,8 @@ class ChunkPipeline:
                     pl.gated = gates[0]
                 pred = SC.simulate(lengths, W, plans, costs)
             else:
-                plans, pred = SC.plan_ring(lengths, W, costs, cap, policies, gates, offload=offload)
+                plans, pred = SC.plan_ring(lengths, W, costs, cap, policies, gates, offload=offload,
+                                           max_held=max_held)
             cache[key] = (plans, pred)
         self.prediction = cache[key][1]
         plans = cache[key][0]
@@ -719,7 +747,9 @@ class ChunkPipeline:
         ``gather_dense`` the depth maps through a second one."""
         n = len(chunks)
         W = self.world
-        if W > 1:
+        # _collective_gather (tests): the collective form at W = 1 too, so one GPU runs
+        # the RCCL all-gathers on device buffers (tests/test_gpu_pipeline.py)
+        if W > 1 or self.__dict__.get("_collective_gather"):
             per_chunk = self._all_gather_chunks(mine, dense, chunks, B)
         else:
             per_chunk = mine

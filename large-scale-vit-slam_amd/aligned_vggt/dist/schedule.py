@@ -166,6 +166,20 @@ def make_jobs(groups: Sequence[Sequence[int]], policy: str) -> List[Job]:
     raise ValueError(policy)
 
 
+def held_peak(jobs: Sequence[Job]) -> int:
+    """Most chunks whose core results wait on the device for their DPT job at
+    any point of one rank's job list ("end" holds every core until the last
+    encode; "lag" at most two groups; "with" none)."""
+    held = peak = 0
+    for kind, g in jobs:
+        if kind == "core":
+            held += len(g)
+            peak = max(peak, held)
+        elif kind == "dense":
+            held -= len(g)
+    return peak
+
+
 def split_groups(own: Sequence[int], lengths: Sequence[int], sizes: Sequence[int]) -> List[List[int]]:
     """Cut the rank's longest equal-length run by ``sizes``; other runs (a
     tail chunk of another length) become groups of their own."""
@@ -267,11 +281,16 @@ _POLICIES = ("with", "lag", "end")
 
 def plan_ring(lengths: Sequence[int], W: int, costs: Optional[RingCosts] = None, cap: int = 3,
               policies: Sequence[str] = _POLICIES, gates: Sequence[bool] = (True, False),
-              sweeps: int = 2, offload: bool = True, refine: bool = True) -> Tuple[List[RankPlan], Prediction]:
+              sweeps: int = 2, offload: bool = True, refine: bool = True,
+              max_held: Optional[int] = None) -> Tuple[List[RankPlan], Prediction]:
     """Per-rank plans minimising the predicted sequence time: each rank's
     longest equal-length run is cut into groups of <= cap chunks (every
     composition tried) under each DPT placement policy, gated or not, rank by rank, a few
-    coordinate-descent sweeps from the best uniform choice.  Then (offload)
+    coordinate-descent sweeps from the best uniform choice.  ``max_held``
+    bounds device memory: no rank's plan may hold more than that many chunks'
+    core results waiting for their DPT job (``held_peak``; the caller derives
+    it from a byte budget), so a long sequence falls back from "end" to "lag"
+    or "with" instead of growing without bound.  Then (offload)
     alignments move, one at a time, from the rank that finishes last to the
     ranks that finish first while the prediction improves: 43 chunks over 8
     ranks leave two ranks six chunks, and their alignments' gate pauses are
@@ -285,7 +304,13 @@ def plan_ring(lengths: Sequence[int], W: int, costs: Optional[RingCosts] = None,
     for r in range(W):
         runs = runs_of(owns[r], lengths)
         m = max((len(x) for x in runs), default=0)
-        options.append([(c, p, gt) for c in candidate_sizes(m, cap) for p in policies for gt in gates])
+        opts = [(c, p, gt) for c in candidate_sizes(m, cap) for p in policies for gt in gates]
+        if max_held is not None:
+            fits = [o for o in opts
+                    if held_peak(make_jobs(split_groups(owns[r], lengths, o[0]), o[1])) <= max_held]
+            # "with" holds nothing, so it always fits
+            opts = fits or [(c, "with", gt) for c in candidate_sizes(m, cap) for gt in gates]
+        options.append(opts)
 
     def build(choice):
         return [RankPlan(make_jobs(split_groups(owns[r], lengths, c), p), c, p, gt)
@@ -304,7 +329,11 @@ def plan_ring(lengths: Sequence[int], W: int, costs: Optional[RingCosts] = None,
             m = sum(c)
             mine = max((len(x) for x in runs_of(owns[r], lengths)), default=0)
             cc = c if mine == m else _fit(c, mine, cap)
-            choice.append((cc, p, gt))
+            if max_held is not None and held_peak(make_jobs(split_groups(owns[r], lengths, cc), p)) > max_held:
+                p_r = "with"  # the fitted composition of a longer run may hold one chunk more
+            else:
+                p_r = p
+            choice.append((cc, p_r, gt))
         sc, pr = score(choice)
         if p not in uniform or sc < uniform[p][0]:
             uniform[p] = (sc, choice, pr)

@@ -59,7 +59,7 @@ def synthetic_images(B: int, S: int, H: int, W: int, seed: int = 1234, device="c
 
 
 @torch.no_grad()
-def condition_pose_outputs_(model: nn.Module) -> nn.Module:
+def condition_pose_outputs_(model: nn.Module, translation: float = 0.0) -> nn.Module:
     """Put the random-init pose decoders in a well-conditioned regime.
 
     With N(0, 0.02) weights the camera head / alignment decoders emit
@@ -67,11 +67,16 @@ def condition_pose_outputs_(model: nn.Module) -> nn.Module:
     quaternions are normalised before use, data.py:45, rotation.quat_to_mat)
     is then ill-conditioned.  Trained models emit near-unit quaternions; we
     emulate that by biasing the last decoder layers towards the identity
-    rotation and a ~1 rad field of view.  Only biases change."""
+    rotation and a ~1 rad field of view.  ``translation`` (per refinement
+    iteration, along the optical axis) does the same for the camera
+    translation, which otherwise sits near zero, where its relative error is
+    ill-conditioned; 0 keeps the earlier fixtures' init.
+    Only biases change."""
     cam = getattr(model, "camera_head", None)
     if cam is not None:
         b = cam.pose_branch.fc2.bias
         b.zero_()
+        b[2] = translation  # T_z: 4 x translation after the 4 refinement iterations
         b[6] = 0.25  # quat w, accumulated over 4 refinement iterations
         b[7:9] = 0.25  # FoV (h, w) -> ~1 rad after 4 iterations
     ah = getattr(model, "alignment_head", None)

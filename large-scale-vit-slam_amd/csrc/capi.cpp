@@ -27,7 +27,8 @@ int g_vggt_conv_pf2 = env_or("VGGT_CONV_PF2", 1);
 int g_vggt_linear_one_launch = env_or("VGGT_LINEAR_ONE_LAUNCH", 1);
 int g_vggt_linear_split_k = env_or("VGGT_LINEAR_SPLIT_K", 128);
 int g_vggt_linear_wk = env_or("VGGT_LINEAR_WK", 64);
-int g_vggt_gemm_balance = env_or("VGGT_GEMM_BALANCE", 0);  // align_chunk 2.87 -> 2.58 ms (profiles/r10/align_*)
+int g_vggt_gemm_balance = env_or("VGGT_GEMM_BALANCE", 0);  // whole rounds persistent + tail on 128x128: bitwise equal but
+// slower in the model (aggregator step 99.4-99.96 vs 98.7-99.0 ms, profiles/r10/ab_r10n_head_*.json), so off
 
 extern "C" int vggt_tune(int knob, int value) {
   int prev;

@@ -56,6 +56,46 @@ def test_aggregator_headline_chunk_reduced_depth(cuda):
         assert e < 4e-3, e  # measured 1.7e-3 (round 3); 2x that, rounded up
 
 
+def test_aggregator_headline_chunk_full_depth(cuda):
+    """the headline config end to end -- the full HIP
+    Aggregator (DINOv2 x 24, 24 frame + 24 global blocks, 21,984-token global
+    attention) on one 16 x 518^2 chunk -- against the CPU oracle run at the
+    same depth and size in both tiers (tests/golden/configs1_full.npz, a
+    strided subsample of layers 4/11/17/23, made by
+    tests/golden/gen_configs1_full.py; featureAligned_vggt.py:78-82).  bf16
+    error compounding through 24 global-attention layers at nk = 21,984 (the
+    offset-free softmax's range guard, P rounded to bf16, fp32 row sums over
+    21,984 keys) is what this measures.  Bars per kept layer: the HIP output
+    no further from the fp32 oracle, and from the bf16 oracle, than 1.25x the
+    oracle's own bf16-vs-fp32 spread."""
+    import numpy as np
+    from aligned_vggt.backbone.aggregator import Aggregator
+    from aligned_vggt.utils.synthetic import synthetic_images, synthetic_init_
+    ref = np.load(os.path.join(os.path.dirname(__file__), "golden", "configs1_full.npz"))
+    keep = tuple(int(x) for x in ref["keep"])
+    frames = [int(x) for x in ref["frames"]]
+    ts, cs = int(ref["token_stride"]), int(ref["channel_stride"])
+    agg = Aggregator()
+    synthetic_init_(agg, seed=int(ref["weight_seed"]))
+    img = synthetic_images(1, 16, 518, 518, seed=int(ref["image_seed"]))
+    agg = agg.to(cuda)
+    with torch.no_grad():
+        outs, psi = agg(img.to(cuda), keep_layers=keep)
+    torch.cuda.synchronize()
+    assert psi == 5 and len(outs) == len(keep)
+    got = torch.stack([o[0, frames, ::ts, ::cs].float().cpu() for o in outs])
+    del outs
+    rb, rf = torch.from_numpy(ref["bf16"]), torch.from_numpy(ref["fp32"])
+    assert got.shape == rb.shape, (got.shape, rb.shape)
+    assert torch.isfinite(got).all()
+    for li, layer in enumerate(keep):
+        e_b, e_f, sp = _rel(got[li], rb[li]), _rel(got[li], rf[li]), _rel(rb[li], rf[li])
+        print(f"configs[1] full depth, layer {layer}: hip vs bf16 oracle {e_b:.3e}, hip vs fp32 oracle {e_f:.3e}, "
+              f"oracle bf16 vs fp32 {sp:.3e} (full tensor {float(ref['spread_full'][li]):.3e})")
+        assert e_f <= 1.25 * sp, (layer, e_f, sp)
+        assert e_b <= 1.25 * sp, (layer, e_b, sp)
+
+
 def test_vkitti_sequence_with_tail_reduced_depth(cuda, monkeypatch):
     """36 frames of 154 x 518, chunk 16 / overlap 4 -> chunks [0-15], [12-27] and
     a 12-frame tail [24-35]: HIP model through apply_sequence_to_model (grouped
@@ -221,3 +261,97 @@ def test_configs2_sequence_518_reduced_depth(cuda):
         assert e[k] < bar, (k, e[k], bar)
     for k in ("pose_T", "pose_quat", "pose_fov"):
         assert e[k] < 1.5 * spread[k], (k, e[k], spread[k])
+
+
+def _synthetic_w2c(S, seed=7):
+    """GT trajectory of SURVEY.md §8d: yaw random walk (sigma 0.5 deg / frame),
+    1 unit forward per frame, seed 7; w2c (1, S, 3, 4) (OpenCV, README.md:127)."""
+    g = torch.Generator().manual_seed(seed)
+    yaw = torch.cumsum(torch.randn(S, generator=g) * 0.0087, 0)
+    c2w = torch.eye(4).repeat(S, 1, 1)
+    c2w[:, 0, 0], c2w[:, 0, 2], c2w[:, 2, 0], c2w[:, 2, 2] = yaw.cos(), yaw.sin(), -yaw.sin(), yaw.cos()
+    c2w[:, :3, 3] = torch.cumsum(torch.stack([yaw.sin(), torch.zeros(S), yaw.cos()], -1), 0)
+    return torch.linalg.inv(c2w)[:, :3, :][None]
+
+
+def test_vkitti_sequence_ate_rpe_parity(cuda, monkeypatch):
+    """the metric's "ATE/RPE parity vs ref" at the
+    configs[3]/[4] chunk shape -- 38 frames of 154 x 518, chunk 16 / overlap 4
+    -> chunks [0-15], [12-27] and a 14-frame tail [24-37]; memory 8, reduced
+    aggregator depth (4 + DINOv2 1) -- through apply_sequence_to_model with the
+    'scale_from_poses' GT alignment (training_metrics.py:239-262,
+    alignment.py:206-242), against the oracle chunk loop in both tiers.  The
+    camera head's translation is conditioned (4 x 0.25 along the optical axis)
+    so its relative error is well-posed.  ATE RMSE (trajectory_metrics.py:28-77)
+    and RPE trans / rot (:154-223) of the HIP trajectory against the synthetic
+    GT must match the bf16 oracle's."""
+    from aligned_vggt.backbone.aggregator import Aggregator
+    from aligned_vggt.dist.pipeline import apply_sequence_to_model
+    from aligned_vggt.eval import AbsoluteTrajectoryError, RelativePoseError, poses_c2w_from_predictions
+    from aligned_vggt.models import featureAligned_vggt as FAmod
+    from aligned_vggt.models.featureAligned_vggt import FeatureAlignedVGGT
+    from aligned_vggt.utils import alignment as A
+    from aligned_vggt.utils.synthetic import condition_pose_outputs_, synthetic_images, synthetic_init_
+    N, w, ov, H, W = 38, 16, 4, 154, 518
+    chunks = O.generate_chunks(N, w, ov)
+    assert [len(c) for c in chunks] == [16, 16, 14]  # a shorter tail chunk (data.py:188-190)
+    monkeypatch.setattr(FAmod, "Aggregator", lambda **kw: Aggregator(depth=4, dino_depth=1, **kw))
+    m = FeatureAlignedVGGT(enable_point=False, enable_track=False, num_memory_tokens=8)
+    m.intermediate_layer_indices = [0, 1, 2, 3]
+    synthetic_init_(m, seed=17)
+    condition_pose_outputs_(m, translation=0.25)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(cuda).eval()
+    imgs = synthetic_images(1, N, H, W, seed=41)
+    extr = _synthetic_w2c(N)
+    got = apply_sequence_to_model({"images": imgs.to(cuda), "extrinsics": extr.to(cuda)}, m, [w], [ov],
+                                  "chunk_overlap", "scale_from_poses")
+    torch.cuda.synchronize()
+    agg_kw = {"keep": (0, 1, 2, 3), "depth": 4, "dino_depth": 1}
+
+    def oracle(bf16):
+        ctx = None
+        with torch.no_grad():
+            for ids in chunks:
+                ctx = O.feature_aligned_forward(sd, imgs[:, ids], ov, ctx, bf16=bf16, agg_kwargs=agg_kw)
+        pe = torch.cat([p[:, (ov if i else 0):] for i, p in enumerate(ctx["pose_enc"])], 1)
+        pred = {"pose_enc": pe}
+        A.scale_alignment_from_poses(pred, {"extrinsics": extr})
+        return ctx, pred["pose_enc"]
+
+    (ctx_b, pe_b), (ctx_f, pe_f) = oracle(True), oracle(False)
+    pe = got["pose_enc"].cpu()
+    assert pe.shape == (1, N, 9)
+
+    def parts(p, ctx):
+        return {"chunk_sim3": ctx["chunk_sim3_alignment_enc"] if ctx is not None else None,
+                "pose_T": p[..., :3], "pose_quat": p[..., 3:7], "pose_fov": p[..., 7:]}
+
+    e = {"chunk_sim3": _rel(got["chunk_sim3_alignment_enc"], ctx_b["chunk_sim3_alignment_enc"]),
+         "frame_se3": _rel(got["frame_se3_alignment_enc"], ctx_b["frame_se3_alignment_enc"]),
+         "pose_T": _rel(pe[..., :3], pe_b[..., :3]), "pose_quat": _quat_rel(pe[..., 3:7], pe_b[..., 3:7]),
+         "pose_fov": _rel(pe[..., 7:], pe_b[..., 7:])}
+    spread = {"chunk_sim3": _rel(ctx_f["chunk_sim3_alignment_enc"], ctx_b["chunk_sim3_alignment_enc"]),
+              "frame_se3": _rel(ctx_f["frame_se3_alignment_enc"], ctx_b["frame_se3_alignment_enc"]),
+              "pose_T": _rel(pe_f[..., :3], pe_b[..., :3]), "pose_quat": _quat_rel(pe_f[..., 3:7], pe_b[..., 3:7]),
+              "pose_fov": _rel(pe_f[..., 7:], pe_b[..., 7:])}
+    _report("154x518 ATE/RPE sequence", e, spread)
+
+    def metrics(pose_enc):
+        p, g = poses_c2w_from_predictions(pose_enc.cpu(), extr, (H, W))
+        ate, rpe = AbsoluteTrajectoryError(), RelativePoseError()
+        ate.update(p[0], g[0])
+        rpe.update(p[0], g[0])
+        return {k: float(v) for k, v in {**ate.compute(), **rpe.compute()}.items()}
+
+    m_hip, m_b, m_f = metrics(pe), metrics(pe_b), metrics(pe_f)
+    print("ATE/RPE hip", m_hip, "\nATE/RPE oracle bf16", m_b, "\nATE/RPE oracle fp32", m_f)
+    assert e["chunk_sim3"] < 1e-3 and e["frame_se3"] < 1e-3, e  # the north star's 1e-3
+    for k, bar in {"pose_T": 2e-2, "pose_quat": 2e-2, "pose_fov": 2e-2}.items():
+        assert e[k] < bar, (k, e[k], bar)
+    for k in m_b:
+        d_hip, d_sp = abs(m_hip[k] - m_b[k]), abs(m_f[k] - m_b[k])
+        rel = d_hip / max(abs(m_b[k]), 1e-12)
+        print(f"{k}: hip {m_hip[k]:.6g} oracle bf16 {m_b[k]:.6g} fp32 {m_f[k]:.6g} | hip-vs-bf16 rel {rel:.2e}, "
+              f"|hip-bf16| / |fp32-bf16| = {d_hip / max(d_sp, 1e-30):.2f}")
+        assert rel < 2e-2, (k, m_hip, m_b)

@@ -140,3 +140,76 @@ def test_pipeline_streams_are_shared(cuda):
         seen.add((s.cuda_stream, side.cuda_stream))
         pipe.close()
     assert len(seen) == 1, seen
+
+
+def test_pipeline_close_then_new_pipeline_reuses_shared_streams(cuda, monkeypatch):
+    """The r9b fault: on the fdd8166 tree ``close()`` destroyed
+    the pipeline's HIP streams while the caching allocator still held blocks
+    handed out on them, and the next pipeline's run crashed (segfault in this
+    file's overlapped-schedule test).  Streams are process-wide since 3eb7faf;
+    this is the exact sequence: run, close, a second pipeline on the same
+    shared streams, run again -- both bitwise the sequential loop."""
+    from aligned_vggt.dist.pipeline import ChunkPipeline, apply_sequence_to_model
+    from aligned_vggt.utils.synthetic import synthetic_images
+    m = _model(cuda, monkeypatch)
+    N_, w, ov, H, W = 20, 8, 2, 56, 70
+    imgs = synthetic_images(1, N_, H, W, seed=5).to(cuda)
+    ref = apply_sequence_to_model({"images": imgs}, m, [w], [ov], "chunk_overlap", None)
+    P1 = 6 + (H // 14) * (W // 14)
+    streams = []
+    for _ in range(2):
+        pipe = ChunkPipeline(m, device=cuda, gather_dense=True, encode_group=2, overlap_align=True)
+        pipe.plan_gates = (True,)
+        got = pipe.run(imgs, w, ov, token_dims=(P1, 1024), memory_shape=(1, 8, 512))
+        streams.append(pipe._encode_stream().cuda_stream)
+        pipe.close()
+        del pipe
+        torch.cuda.synchronize()
+        for k in ("pose_enc", "chunk_sim3_alignment_enc", "frame_se3_alignment_enc", "depth"):
+            assert torch.equal(got[k].cpu(), ref[k].cpu()), k
+        del got
+    assert streams[0] == streams[1]
+
+
+def test_collective_gather_over_rccl_world1(cuda, monkeypatch):
+    """the end-of-sequence gathers -- the small per-chunk slab,
+    the dense-map flags and the dense depth maps (gather_dense) -- through
+    ``all_gather_into_tensor`` on DEVICE buffers of an ``nccl`` (RCCL) process
+    group, world size 1 on the one GPU of the test box.  Results equal the
+    sequential loop bitwise (the gather only moves bytes)."""
+    import socket
+
+    import torch.distributed as dist
+    from aligned_vggt.dist.pipeline import ChunkPipeline, apply_sequence_to_model
+    from aligned_vggt.utils.synthetic import synthetic_images
+    assert not dist.is_initialized()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=cuda if cuda.index is not None else torch.device("cuda", 0))
+    try:
+        assert dist.get_backend() == "nccl"
+        m = _model(cuda, monkeypatch)
+        N_, w, ov, H, W = 20, 8, 2, 56, 70
+        imgs = synthetic_images(1, N_, H, W, seed=8).to(cuda)
+        ref = apply_sequence_to_model({"images": imgs}, m, [w], [ov], "chunk_overlap", None)
+        P1 = 6 + (H // 14) * (W // 14)
+        with ChunkPipeline(m, device=cuda, gather_dense=True, encode_group=2, overlap_align=True) as pipe:
+            assert pipe.world == 1 and pipe._comm_device.type == "cuda"
+            pipe._collective_gather = True
+            calls = []
+            real = dist.all_gather_into_tensor
+
+            def spy(out, inp, group=None, **kw):
+                calls.append((tuple(out.shape), out.device.type, inp.device.type))
+                return real(out, inp, group=group, **kw)
+
+            monkeypatch.setattr(dist, "all_gather_into_tensor", spy)
+            got = pipe.run(imgs, w, ov, token_dims=(P1, 1024), memory_shape=(1, 8, 512))
+            torch.cuda.synchronize()
+        assert len(calls) == 3 and all(d == "cuda" and i == "cuda" for _, d, i in calls), calls
+        for k in ("pose_enc", "chunk_sim3_alignment_enc", "frame_se3_alignment_enc", "depth", "depth_conf"):
+            assert torch.equal(got[k].cpu(), ref[k].cpu()), k
+    finally:
+        dist.destroy_process_group()

@@ -96,7 +96,7 @@ def test_linear_f32_split_k_one_launch(N, M, Nn, K, epi, act, split_k):
                                              (16, 6144, 2048, 3, 1), (40, 512, 1024, 2, 1), (17, 96, 200, 3, 0),
                                              (130, 1024, 2048, 2, 0)])
 def test_linear_f32_in_workgroup_split(N, M, Nn, K, epi, act, wk):
-    """M <= 64 on the in-workgroup split-K form (VGGT_TUNE_LINEAR_WK: 2..16
+    """M <= 64 on the in-workgroup split-K form (VGGT_TUNE_LINEAR_WK: 2..8
     waves on 16 columns, partials summed in LDS in wave order): bitwise run to
     run, within fp32 rounding of an fp64 reference (ragged K and N, the SiLU
     input, the GELU / LayerScale-residual epilogues), and close to the

@@ -115,3 +115,32 @@ def test_refine_never_worse_and_keeps_ownership(W):
     assert len(ar) == len(L) and all(0 <= a < W for a in ar)
     assert all(pl.align_rank == ar for pl in plans)
     assert SC.simulate(L, W, plans, c).total_ms == pytest.approx(pr.total_ms)
+
+
+def test_held_peak_by_policy():
+    gs = [[0, 1], [2, 3], [4]]
+    assert SC.held_peak(SC.make_jobs(gs, "with")) == 0
+    assert SC.held_peak(SC.make_jobs(gs, "lag")) == 4  # core(2,3) queued before dense(0,1)
+    assert SC.held_peak(SC.make_jobs(gs, "end")) == 5
+
+
+def test_planner_memory_bound_on_long_sequence():
+    """the one-rank plan may pick "end" (every core result held until
+    the DPT jobs at the end), whose device memory grows with the sequence.  With
+    max_held the plan of a long sequence holds at most that many chunks, and an
+    unbounded plan shows the bound bites (2,048 frames -> 171 chunks, one rank)."""
+    lengths = [len(c) for c in generate_chunks(2048, "chunk_overlap", 16, 4)]
+    assert len(lengths) == 171
+    costs = SC.DEFAULT_COSTS
+    free, _ = SC.plan_ring(lengths, 1, costs, 3, ("with", "lag", "end"), (False,), sweeps=1)
+    assert SC.held_peak(free[0].jobs) > 12  # unbounded, the planner holds many chunks
+    for bound in (3, 12):
+        plans, pr = SC.plan_ring(lengths, 1, costs, 3, ("with", "lag", "end"), (False,), sweeps=1, max_held=bound)
+        assert SC.held_peak(plans[0].jobs) <= bound
+        covered = sorted(i for kind, g in plans[0].jobs if kind in ("enc", "core") for i in g)
+        assert covered == list(range(len(lengths)))
+        assert pr.total_ms >= 0.0
+    # at W = 8 every rank's plan stays under the bound too
+    lengths = [len(c) for c in generate_chunks(512, "chunk_overlap", 16, 4)]
+    plans, _ = SC.plan_ring(lengths, 8, costs, 3, max_held=3, offload=False)
+    assert all(SC.held_peak(pl.jobs) <= 3 for pl in plans)
