@@ -557,9 +557,10 @@ def _ring_model(model, pipe, seq, S, ov, rec, t1_ms):
     events on one stream, median of 3 after a warm-up; t_align alone / beside
     a gated encode / ungated from the recurrence probe; the encode time one
     alignment costs its rank (t_pause) from the W = 1 overlapped sequences
-    minus their plan's job time.  The baton hop (28 MB over one xGMI link) is
-    not measurable on one GPU: 0.25 ms is modelled.  T1 = this run's
-    measured single-rank sequence."""
+    minus their plan's job time.  The baton hop and a moved alignment's ship
+    are not measurable on one GPU: they are priced from their bytes at an
+    assumed link rate, reported under ``assumed``.  T1 = this run's measured
+    single-rank sequence."""
     import statistics
     from aligned_vggt.dist import schedule as SC
     from aligned_vggt.utils.data import generate_chunks
@@ -621,11 +622,16 @@ def _ring_model(model, pipe, seq, S, ov, rec, t1_ms):
             costs.t_pause = round(tp, 3)
         else:
             costs.t_pause_ungated = round(tp, 3)
-    pred = SC.predict_scaling(lengths, costs)
+    pred = SC.predict_scaling(lengths, costs, offload=pipe.plan_offload)
     for W, d in pred.items():
         d["T1_over_TW"] = round(t1_ms / d["T_ms"], 2)
     w1, _ = SC.plan_ring(lengths, 1, costs, cap, pipe.plan_policies, (True,))
     return {"costs": costs.to_json(), "T1_measured_ms": round(t1_ms, 1), "predicted": pred,
+            # NOT measured: the two point-to-point transfers, priced from their bytes (the first
+            # 8-GPU run recalibrates them: VGGT_RING_COSTS=<its line> with measured hop / ship)
+            "assumed": {"hop_ms": costs.hop, "baton_bytes": baton_b, "ship_ms": costs.ship, "ship_bytes": ship_b,
+                        "link_GB_per_s": 100.0, "per_transfer_us": 20.0,
+                        "offload_default": pipe.plan_offload},
             "check_w1_overlapped_gated": {"predicted_ms": round(SC.simulate(lengths, 1, w1, costs).total_ms, 1),
                                           "measured_ms": rec["sequence_ms_under_load"],
                                           "note": "t_pause is calibrated on this run, so this agrees by construction "

@@ -622,6 +622,15 @@ int vggt_batch_dot_f32(const float* a, const float* c, int64_t bs, int B, int64_
  * after the loop, s_memrealtime (100 MHz) before / after.  sink: nwg * 256 floats, never read. */
 int vggt_mfma_probe(unsigned long long* stamps, float* sink, const void* operands, int nwg, int iters, void* stream);
 
+/* Attention segment stamps (diagnostic; VERDICT r5: where the global attention's waits go).  Runs the
+ * default D = 64 forward (variant 33, the 8- / 4-wave choice of vggt_attention_fwd, o written as there) with
+ * s_memtime stamps at each tile's boundaries; per wave (index (blockIdx * NW + wave) * 8) the cycle sums
+ * [2] the tile's work up to its last LDS read, [3] end-of-tile vmcnt(0), [4] barrier ([0], [1], [5] unused),
+ * [6] the wave's final s_memtime (low 32 bits); every wave runs ceil(nk / 64) tiles.  stamps: nwg * NW * 8 entries, NW = 8 for nq >= 4096 else 4. */
+int vggt_attention_stamps(const void* q, int64_t ldq, int64_t q_bstride, const void* k, int64_t ldk, int64_t k_bstride,
+                          const void* v, int64_t ldv, int64_t v_bstride, void* o, int64_t ldo, int64_t o_bstride,
+                          unsigned long long* stamps, int batch, int heads, int nq, int nk, float scale, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

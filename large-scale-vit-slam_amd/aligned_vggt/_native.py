@@ -31,6 +31,8 @@ _SIGS = {
     "vggt_tune": [_i, _i],
     "vggt_set_stream_config": [_vp, _i, _i],
     "vggt_mfma_probe": [_vp, _vp, _vp, _i, _i, _vp],
+    "vggt_attention_stamps": [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i, _i, _i, _i,
+                              _f, _vp],
     "vggt_gemm_bf16": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _vp, _i64, _vp, _vp, _i64, _vp],
     "vggt_gemm_qkv": [_vp, _i64, _vp, _i64, _vp, _i, _i, _i, _i, _vp, _i64, _vp, _vp, _vp, _vp, _f, _i, _vp, _i, _vp,
                       _vp, _i, _vp],
@@ -385,6 +387,21 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, o: torch.Tensor
 
     rc = EVENT_HOOK(tag, call) if (EVENT_HOOK is not None and tag is not None) else call()
     _check(rc, "vggt_attention_fwd")
+
+
+def attention_stamps(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, o: torch.Tensor, batch: int, heads: int,
+                     nq: int, nk: int, q_bstride: int, k_bstride: int, o_bstride: int) -> torch.Tensor:
+    """Diagnostic (vggt_attention_stamps): the default D = 64 forward with per-wave
+    s_memtime cycle sums of its tile segments; returns (nwg * NW, 8) int64."""
+    _dev(q, "attention_stamps")
+    nw = 8 if nq >= 4096 else 4
+    nwg = ((nq + nw * 32 - 1) // (nw * 32)) * heads * batch
+    st = torch.zeros(nwg * nw, 8, dtype=torch.int64, device=q.device)
+    rc = lib().vggt_attention_stamps(_p(q), _ld(q), q_bstride, _p(k), _ld(k), k_bstride, _p(v), _ld(v), k_bstride,
+                                     _p(o), _ld(o), o_bstride, _p(st), batch, heads, nq, nk, float(64 ** -0.5),
+                                     _stream())
+    _check(rc, "vggt_attention_stamps")
+    return st
 
 
 def patch_im2col(images: torch.Tensor, patch: int, mean, std, out: torch.Tensor) -> None:

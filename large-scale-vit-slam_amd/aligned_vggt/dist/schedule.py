@@ -489,16 +489,18 @@ def enqueue_order(plan: RankPlan, own: Sequence[int], rank: Optional[int] = None
     return out
 
 
-def predict_scaling(lengths: Sequence[int], costs: RingCosts, worlds=(1, 2, 4, 8)) -> dict:
-    """Predicted sequence time at each W (the planner's plans) and, for
-    comparison, the round-4 schedule's."""
+def predict_scaling(lengths: Sequence[int], costs: RingCosts, worlds=(1, 2, 4, 8), offload: bool = False) -> dict:
+    """Predicted sequence time at each W with the plans the pipeline runs by
+    default (``offload``: alignments moved off their owner, VGGT_RING_OFFLOAD),
+    the other offload setting beside it, and the round-4 schedule's."""
     out = {}
     for W in worlds:
-        plans, pr = plan_ring(lengths, W, costs)
-        _, pr_no = plan_ring(lengths, W, costs, offload=False) if W > 1 else (None, pr)
+        plans, pr = plan_ring(lengths, W, costs, offload=offload)
+        _, pr_alt = plan_ring(lengths, W, costs, offload=not offload) if W > 1 else (None, pr)
         leg = simulate(lengths, W, legacy_plans(lengths, W), costs)
         moved = [i for i, a in enumerate(plans[0].align_rank) if a != i % W] if plans[0].align_rank else []
-        out[str(W)] = {"T_ms": round(pr.total_ms, 1), "T_ms_no_offload": round(pr_no.total_ms, 1),
+        out[str(W)] = {"T_ms": round(pr.total_ms, 1),
+                       ("T_ms_with_offload" if not offload else "T_ms_no_offload"): round(pr_alt.total_ms, 1),
                        "T_ms_round4_schedule": round(leg.total_ms, 1), "alignments_moved": moved,
                        "plans": [{"groups": [list(g) for k, g in pl.jobs if k in ("enc", "core")],
                                   "policy": pl.policy, "gated": pl.gated} for pl in plans[:min(W, 3)]]}

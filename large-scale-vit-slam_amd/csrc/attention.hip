@@ -93,7 +93,11 @@ __device__ __forceinline__ int v_swz(int row, int chunk) {
 // fragment reads before the QK^T MFMAs, bit 1 = four-chain row max, bit 2 =
 // four partial row sums, bit 3 = row sums on the matrix core (an all-ones
 // V^T block times P^T: 4 extra MFMAs per tile replace 32 VALU adds per lane;
-// the sum is then over the bf16-rounded P that also feeds P.V).
+// the sum is then over the bf16-rounded P that also feeds P.V).  Bit 10
+// (1024, diagnostic, on top of 33): s_memtime stamps per tile segment, summed
+// per wave into a.lse reinterpreted as unsigned long long[nwg][NW][STAMP_N]
+// (vggt_attention_stamps; the kernel writes no lse then).
+constexpr int STAMP_N = 8;
 template <int D, int NW, int VAR>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
   constexpr int BQ = NW * 32;            // query rows per workgroup (32 per wave)
@@ -104,7 +108,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
   constexpr int RPI = 1024 / ROWB;       // rows per 1-KiB DMA instruction
   constexpr int CPR = ROWB / 16;         // 16-B chunks per row
   constexpr int IPW = TILEB / 1024 / NW;  // DMA instructions per wave per operand
-  constexpr int NSLOT = (VAR & 16) ? 3 : 2;  // K|V tile slots (3: pipelined QK^T)
+  constexpr int NSLOT = (VAR & (16 | 512)) ? 3 : 2;  // K|V tile slots (3: pipelined QK^T / DMA two ahead)
   __shared__ __attribute__((aligned(16))) char smem[NSLOT * 2 * TILEB];
 
   const int lane = threadIdx.x & 63;
@@ -205,6 +209,23 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
   bool zero_off = false;
   const float c = a.c;
   const int nt = (a.nk + BKV - 1) / BKV;
+  // VAR & 1024: per-wave cycle sums of the tile segments (s_memtime, one scalar
+  // statement with its lgkmcnt(0)); 32-bit sums, no tile counter (the host
+  // knows the tile count): so instrumented, the kernel keeps the default's 113
+  // VGPRs and occupancy (a per-tile counter, VGPR-pinned sums or scheduling
+  // barriers around the stamps each pushed it to 119-153)
+  uint32_t st_acc[STAMP_N] = {}, st_prev = 0;
+#define VGGT_SEG(i)                                                                                  \
+  do {                                                                                               \
+    if constexpr (VAR & 1024) {                                                                      \
+      /* no sched_barrier: it pushed the kernel to 150 VGPRs */                                     \
+      unsigned long long now_;                                                                       \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(now_)::"memory");                     \
+      if ((i) >= 0) st_acc[(i) >= 0 ? (i) : 0] += (uint32_t)now_ - st_prev;                          \
+      st_prev = (uint32_t)now_;                                                                      \
+      /* no sched_barrier: it pushed the kernel to 150 VGPRs */                                     \
+    }                                                                                                \
+  } while (0)
 
   struct S2 {
     f32x16 v[2];
@@ -577,6 +598,40 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
       if (t + 2 >= nt) break;
       step(I2{}, I0{}, I1{}, t + 2);
     }
+  } else if constexpr (VAR & 512) {
+    // Three K|V slots, the DMA two tiles ahead: tile t+2 is staged at the start
+    // of tile t (into the slot tile t-1 used, retired by the barrier that ended
+    // tile t-1), and the end of tile t waits only for tile t+1's pieces
+    // (vmcnt counts in order: the 2*IPW pieces of t+2 may stay in flight), so
+    // each tile's loads have two tiles' compute to land instead of one.
+    stage(0, 0);
+    if (nt > 1) stage(1, 1);
+    if (nt > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * IPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    auto step = [&](auto sc, auto sf, auto zc, int t) {
+      if (t + 2 < nt) stage(decltype(sf)::value, t + 2);
+      soft_pv(sc, t, qk(sc), zc);
+      if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * IPW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    };
+    // the offset mode may change only at a multiple of 3 tiles (slot = t % 3)
+    auto run = [&](auto zc, int t0) -> int {
+      for (int t = t0; t < nt; t += 3) {
+        step(I0{}, I2{}, zc, t);
+        if (t + 1 >= nt) break;
+        step(I1{}, I0{}, zc, t + 1);
+        if (t + 2 >= nt) break;
+        step(I2{}, I1{}, zc, t + 2);
+        if constexpr (decltype(zc)::value) {
+          if (!zero_off) return t + 3;
+        }
+      }
+      return nt;
+    };
+    const int t1 = run(std::true_type{}, 0);
+    if (t1 < nt) run(std::false_type{}, t1);
   } else {
     stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -585,19 +640,31 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
     // a per-tile choice between the two exp forms costs ~25 VGPRs at the merge:
     // occupancy 4 -> 3).  Every wave starts in the zero-offset loop and leaves
     // it for good, at a tile pair boundary, once one of its rows took an offset.
+    // VAR & 1024 segments of one tile: [2] the tile's work (DMA issue, QK^T, softmax,
+    // P.V issue, up to its last LDS read), [3] end-of-tile vmcnt(0) wait for the next
+    // tile's DMA, [4] barrier.  (Stamps inside the tile body, between the
+    // DMA issue and QK^T or between the softmax and P.V, serialise what the compiler
+    // overlaps there and pushed the kernel from 113 to 152 VGPRs: not kept.)
     auto run = [&](auto zc, int t0) -> int {
       for (int t = t0; t < nt; t += 2) {
+        VGGT_SEG(-1);
         if (t + 1 < nt) stage(1, t + 1);
         if ((VAR & 256) && (t + 1) * BKV <= a.nk) tile_split(I0{}, zc);
         else soft_pv(I0{}, t, qk(I0{}), zc);
+        VGGT_SEG(2);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        VGGT_SEG(3);
         __syncthreads();
+        VGGT_SEG(4);
         if (t + 1 >= nt) break;
         if (t + 2 < nt) stage(0, t + 2);
         if ((VAR & 256) && (t + 2) * BKV <= a.nk) tile_split(I1{}, zc);
         else soft_pv(I1{}, t + 1, qk(I1{}), zc);
+        VGGT_SEG(2);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        VGGT_SEG(3);
         __syncthreads();
+        VGGT_SEG(4);
         if constexpr (decltype(zc)::value) {
           if (!zero_off) return t + 2;
         }
@@ -620,7 +687,17 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
     l_run = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
   }
   const float inv = 1.f / l_run;
-  if (a.lse && hl == 0 && qrow < a.nq) a.lse[((int64_t)b * a.heads + h) * a.nq + qrow] = m_run + __log2f(l_run);
+  if constexpr (VAR & 1024) {
+    VGGT_SEG(-1);
+    st_acc[6] = st_prev;  // the wave's end (low 32 bits), to place it against the others of its workgroup
+    if (lane == 0) {
+      unsigned long long* out = (unsigned long long*)(void*)a.lse + ((int64_t)blockIdx.x * NW + wave) * STAMP_N;
+#pragma unroll
+      for (int i = 0; i < STAMP_N; ++i) out[i] = st_acc[i];
+    }
+  } else {
+    if (a.lse && hl == 0 && qrow < a.nq) a.lse[((int64_t)b * a.heads + h) * a.nq + qrow] = m_run + __log2f(l_run);
+  }
   if (qrow < a.nq) {
     bf16_t* op = a.o + ((int64_t)b * a.obs + qrow) * a.ldo + h * D;
 #pragma unroll
@@ -962,6 +1039,12 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
     HIP_LAUNCH_CHECK();
     return VGGT_OK;
   }
+  if (g_vggt_attn_variant == 545 && D == 64 && nw != 2 && !a.lse) {  // offset-free, 3 slots, DMA two tiles ahead
+    if (nw == 8) attn_fwd_kernel<64, 8, 545><<<nwg, 512, 0, s>>>(a);
+    else attn_fwd_kernel<64, 4, 545><<<nwg, 256, 0, s>>>(a);
+    HIP_LAUNCH_CHECK();
+    return VGGT_OK;
+  }
   if (g_vggt_attn_variant == 289 && D == 64 && nw != 2 && !a.lse) {  // offset-free, split-tile pipelined
     if (nw == 8) attn_fwd_kernel<64, 8, 289><<<nwg, 512, 0, s>>>(a);
     else attn_fwd_kernel<64, 4, 289><<<nwg, 256, 0, s>>>(a);
@@ -1010,6 +1093,28 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
 // row 4): the exact-score offset-free form (variant 96: no Q prescale, so the
 // backward's recomputed scores match bit for bit) that also stores the per-row
 // log2-sum-exp consumed by vggt_attention_bwd.
+// Diagnostic: the default forward (variant 33, 32x32x16 form, the same 8- / 4-wave
+// choice as vggt_attention_fwd) with s_memtime segment stamps (VAR bit 1024).
+extern "C" int vggt_attention_stamps(const void* q, int64_t ldq, int64_t q_bstride, const void* k, int64_t ldk,
+                                     int64_t k_bstride, const void* v, int64_t ldv, int64_t v_bstride, void* o,
+                                     int64_t ldo, int64_t o_bstride, unsigned long long* stamps, int batch, int heads,
+                                     int nq, int nk, float scale, void* stream) {
+  if (batch <= 0 || heads <= 0 || nq <= 0 || nk <= 0 || !stamps) return VGGT_ERR_SHAPE;
+  if ((ldq | ldk | ldv | ldo) % 8 || ((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) % 16)
+    return VGGT_ERR_ALIGN;
+  if ((uint64_t)nk * (uint64_t)(ldk > ldv ? ldk : ldv) * 2 >= (1ull << 31)) return VGGT_ERR_SHAPE;
+  AttnArgs a{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, ldq, ldk, ldv, ldo,
+             q_bstride, k_bstride, v_bstride, o_bstride, batch, heads, nq, nk,
+             scale * 1.4426950408889634f, (float*)(void*)stamps};
+  const int nw = (g_vggt_attn_waves == 8 && nq >= 4096) ? 8 : 4;
+  const int nwg = ((nq + nw * 32 - 1) / (nw * 32)) * heads * batch;
+  hipStream_t s = (hipStream_t)stream;
+  if (nw == 8) attn_fwd_kernel<64, 8, 33 | 1024><<<nwg, 512, 0, s>>>(a);
+  else attn_fwd_kernel<64, 4, 33 | 1024><<<nwg, 256, 0, s>>>(a);
+  HIP_LAUNCH_CHECK();
+  return VGGT_OK;
+}
+
 extern "C" int vggt_attention_fwd_lse(const void* q, int64_t ldq, int64_t q_bstride, const void* k, int64_t ldk,
                                       int64_t k_bstride, const void* v, int64_t ldv, int64_t v_bstride, void* o,
                                       int64_t ldo, int64_t o_bstride, float* lse, int batch, int heads, int nq, int nk,

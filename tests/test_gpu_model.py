@@ -84,7 +84,7 @@ def test_feature_aligned_two_chunks(models, S, ov, H, W):
     # at overlap 2, the Markley eigen-average of geometry.py:4-37), so they are
     # ALSO held to their distance from the fp32 numerics: within 2x (poses) /
     # 1.5x (points) of the reference's own bf16-vs-fp32 spread.
-    bars = {"chunk_sim3": 1e-3, "frame_se3": 2e-3, "depth": 1.5e-3, "depth_conf": 5e-5, "overlap_tokens": 1.2e-2,
+    bars = {"chunk_sim3": 1e-3, "frame_se3": 1e-3, "depth": 1.5e-3, "depth_conf": 5e-5, "overlap_tokens": 1.2e-2,
             "memory": 6e-3, "points": 3e-2, "pose_enc": 5e-2 if ov > 1 else 3e-2}
     for k, v in e_hip.items():
         assert v < bars[k], (k, v, bars[k], e_hip)
