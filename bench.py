@@ -117,6 +117,17 @@ def cpu_baseline(threads: int):
     committed = _measured_row("C2", threads)
     if committed is not None:
         out["committed_whole_chunk_row"] = committed
+    # the same sample at 4 / 8 / 16 threads on a GPU-box host (scripts/cpu_thread_scaling.py):
+    # how the CPU baseline scales up to the per-command share of 16 threads
+    try:
+        with open(os.path.join(ROOT, "profiles", "r11", "cpu_thread_scaling.json")) as fh:
+            sc = json.load(fh)
+        out["committed_thread_scaling"] = {
+            "host": sc.get("lscpu", {}).get("Model name"),
+            "s_per_chunk_by_threads": {str(r["cores"]): r["s_per_chunk"] for r in sc.get("rows", [])},
+            "source": "profiles/r11/cpu_thread_scaling.json"}
+    except (OSError, ValueError, KeyError):
+        pass
     return out
 
 

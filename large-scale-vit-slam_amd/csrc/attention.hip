@@ -108,7 +108,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
   constexpr int RPI = 1024 / ROWB;       // rows per 1-KiB DMA instruction
   constexpr int CPR = ROWB / 16;         // 16-B chunks per row
   constexpr int IPW = TILEB / 1024 / NW;  // DMA instructions per wave per operand
-  constexpr int NSLOT = (VAR & (16 | 512)) ? 3 : 2;  // K|V tile slots (3: pipelined QK^T / DMA two ahead)
+  constexpr int NSLOT = (VAR & (16 | 512 | 8192)) ? 3 : 2;  // K|V tile slots (3: pipelined QK^T / DMA two ahead / async ring)
   __shared__ __attribute__((aligned(16))) char smem[NSLOT * 2 * TILEB];
 
   const int lane = threadIdx.x & 63;
@@ -117,7 +117,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
   // 8-wave form: the second-dispatched half (waves 4-7) shares each SIMD with
   // an older wave and loses VALU arbitration on every segment; one static
   // priority raise for it (cdna_hip_programming.md T5, static form).
-  if constexpr (NW == 8) {
+  // (VAR & 4096: no priority raise -- re-measured with the segment stamps, r11)
+  if constexpr (NW == 8 && !(VAR & 4096)) {
     if (wave >= 4) __builtin_amdgcn_s_setprio(1);
   }
   const int nqb = (a.nq + BQ - 1) / BQ;
@@ -149,15 +150,23 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
   for (int ks = 0; ks < NKS; ++ks) asm volatile("" : "+v"(qf[ks]));  // retire the Q loads before the loop
 
   // ---- loop-invariant DMA offsets and LDS destinations
-  uint32_t koff[IPW], voff[IPW];
+  // VAR & 2048 (8-wave form): only the priority-1 half (waves 4-7) issues the
+  // tile's LDS-DMA, two pieces per operand each.  Segment stamps (VAR & 1024,
+  // profiles/r11) showed those waves finish each tile ~870 cycles before their
+  // SIMD partners and wait at the barrier, while the partners' tile work is the
+  // tile's critical path: the DMA issue moves off it.
+  constexpr bool DMAH = (VAR & 2048) && NW == 8;
+  constexpr int IPWX = DMAH ? 2 * IPW : IPW;  // pieces per issuing wave per operand
+  const int pbase = DMAH ? (wave >= 4 ? wave - 4 : 0) * IPWX : wave * IPW;
+  uint32_t koff[IPWX], voff[IPWX];
 #pragma unroll
-  for (int i = 0; i < IPW; ++i) {
-    const int row = (wave * IPW + i) * RPI + lane / CPR;
+  for (int i = 0; i < IPWX; ++i) {
+    const int row = (pbase + i) * RPI + lane / CPR;
     const int cp = lane % CPR;
     koff[i] = (uint32_t)(row * a.ldk + k_swz<D>(row, cp) * 8) * 2u;
     voff[i] = (uint32_t)(row * a.ldv + v_swz<D>(row, cp) * 8) * 2u;
   }
-  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem)) + wave * IPW * 1024;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem)) + pbase * 1024;
   // 32-bit scalar descriptor arithmetic (host: nk * ld * 2 < 2^31): a 64-bit
   // "remaining bytes" compare has no SALU form and would run on the VALU
   const int kstep = BKV * (int)a.ldk * 2, vstep = BKV * (int)a.ldv * 2;
@@ -168,10 +177,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
     const int32x4 kr = make_rsrc((const char*)kp + ko, (uint32_t)max(kbytes - ko, 0));
     const int32x4 vr = make_rsrc((const char*)vp + vo, (uint32_t)max(vbytes - vo, 0));
     const uint32_t d = lds0 + buf * 2 * TILEB;
+    if (!DMAH || wave >= 4) {
 #pragma unroll
-    for (int i = 0; i < IPW; ++i) {
-      dma16(kr, koff[i], d + i * 1024);
-      dma16(vr, voff[i], d + TILEB + i * 1024);
+      for (int i = 0; i < IPWX; ++i) {
+        dma16(kr, koff[i], d + i * 1024);
+        dma16(vr, voff[i], d + TILEB + i * 1024);
+      }
     }
   };
 
@@ -632,6 +643,76 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
     };
     const int t1 = run(std::true_type{}, 0);
     if (t1 < nt) run(std::false_type{}, t1);
+  } else if constexpr (VAR & 8192) {
+    // Asynchronous ring (8-wave form with the DMA on the priority half, VAR & 2048):
+    // no per-tile barrier.  Three K|V slots; two LDS counters replace it:
+    //   landed: each issuing wave (4-7) adds 1 once its pieces of tile j >= 2 are in
+    //           LDS (counted vmcnt, tile j+1's pieces may stay in flight), so tile j
+    //           is readable once landed >= 4 (j - 1) (tiles 0 / 1: the prologue barrier);
+    //   done:   every wave adds 1 after its last LDS read of tile j, so the slot of
+    //           tile t-1 may take tile t+2's DMA once done >= 8 t.
+    // A wave may thus run up to one tile ahead of the slowest wave of its workgroup
+    // (the segment stamps: the priority waves finished each tile ~870 cycles early
+    // and waited at the barrier).  Every wait depends only on strictly earlier
+    // tiles' signals, and is bounded: a lost signal ends in wrong output (the tests
+    // compare against fp32 torch), not in a hung wave.
+    static_assert(!(VAR & 8192) || DMAH, "the asynchronous ring needs the DMA on the priority half");
+    __shared__ uint32_t ctr[2];
+    constexpr int P = 2 * IPWX;  // pieces per tile per issuing wave (K and V)
+    const bool issuer = wave >= 4;
+    if (threadIdx.x == 0) {
+      ctr[0] = 0;
+      ctr[1] = 0;
+    }
+    if (issuer) {
+      stage(0, 0);
+      if (nt > 1) stage(1, 1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    auto wait_ge = [&](int idx, uint32_t target) {
+      for (uint32_t spins = 0; spins < (1u << 22); ++spins) {
+        const uint32_t v = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&ctr[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (v >= target) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      asm volatile("" ::: "memory");  // the tile's LDS reads stay after the poll
+    };
+    auto signal = [&](int idx) {
+      if (lane == 0) __hip_atomic_fetch_add(&ctr[idx], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto step = [&](auto sc, auto sf, auto zc, int t) {
+      if (t >= 2) wait_ge(0, 4u * (uint32_t)(t - 1));  // tile t landed
+      if (issuer && t + 2 < nt) {
+        wait_ge(1, 8u * (uint32_t)t);  // every wave is done with tile t-1's slot
+        stage(decltype(sf)::value, t + 2);
+      }
+      soft_pv(sc, t, qk(sc), zc);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot t done
+      signal(1);
+      if (issuer && t + 1 >= 2 && t + 1 < nt) {
+        // tile t+1's pieces (issued at the start of tile t-1) landed; t+2's may fly on
+        if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        signal(0);
+      }
+    };
+    auto run = [&](auto zc, int t0) -> int {
+      for (int t = t0; t < nt; t += 3) {
+        step(I0{}, I2{}, zc, t);
+        if (t + 1 >= nt) break;
+        step(I1{}, I0{}, zc, t + 1);
+        if (t + 2 >= nt) break;
+        step(I2{}, I1{}, zc, t + 2);
+        if constexpr (decltype(zc)::value) {
+          if (!zero_off) return t + 3;
+        }
+      }
+      return nt;
+    };
+    const int t1 = run(std::true_type{}, 0);
+    if (t1 < nt) run(std::false_type{}, t1);
   } else {
     stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1039,6 +1120,34 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
     HIP_LAUNCH_CHECK();
     return VGGT_OK;
   }
+  // Default (round 6): the 8-wave D = 64 form of variant 33 issues its LDS-DMA from the
+  // priority half only (variant 2081): global attention 1,858-1,860 -> 1,814-1,819 us,
+  // aggregator step 97.66-97.75 -> 96.56-97.21 ms, interleaved on one box
+  // (profiles/r11/ab_attn_dma_half.md).  VGGT_ATTN_DMA_HALF=0: every wave issues its piece.
+  static const bool dma_half = getenv("VGGT_ATTN_DMA_HALF") ? atoi(getenv("VGGT_ATTN_DMA_HALF")) != 0 : true;
+  if (dma_half && g_vggt_attn_variant == 33 && D == 64 && nw == 8 && !a.lse) {
+    attn_fwd_kernel<64, 8, 2081><<<nwg, 512, 0, s>>>(a);
+    HIP_LAUNCH_CHECK();
+    return VGGT_OK;
+  }
+  if (g_vggt_attn_variant == 10273 && D == 64 && nw != 2 && !a.lse) {  // 2081 on the asynchronous ring (8-wave form)
+    if (nw == 8) attn_fwd_kernel<64, 8, 10273><<<nwg, 512, 0, s>>>(a);
+    else attn_fwd_kernel<64, 4, 33><<<nwg, 256, 0, s>>>(a);
+    HIP_LAUNCH_CHECK();
+    return VGGT_OK;
+  }
+  if (g_vggt_attn_variant == 4129 && D == 64 && nw != 2 && !a.lse) {  // 33 without the priority raise (8-wave form)
+    if (nw == 8) attn_fwd_kernel<64, 8, 4129><<<nwg, 512, 0, s>>>(a);
+    else attn_fwd_kernel<64, 4, 33><<<nwg, 256, 0, s>>>(a);
+    HIP_LAUNCH_CHECK();
+    return VGGT_OK;
+  }
+  if (g_vggt_attn_variant == 2081 && D == 64 && nw != 2 && !a.lse) {  // 33, DMA by the priority half (8-wave form)
+    if (nw == 8) attn_fwd_kernel<64, 8, 2081><<<nwg, 512, 0, s>>>(a);
+    else attn_fwd_kernel<64, 4, 33><<<nwg, 256, 0, s>>>(a);
+    HIP_LAUNCH_CHECK();
+    return VGGT_OK;
+  }
   if (g_vggt_attn_variant == 545 && D == 64 && nw != 2 && !a.lse) {  // offset-free, 3 slots, DMA two tiles ahead
     if (nw == 8) attn_fwd_kernel<64, 8, 545><<<nwg, 512, 0, s>>>(a);
     else attn_fwd_kernel<64, 4, 545><<<nwg, 256, 0, s>>>(a);
@@ -1093,8 +1202,9 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
 // row 4): the exact-score offset-free form (variant 96: no Q prescale, so the
 // backward's recomputed scores match bit for bit) that also stores the per-row
 // log2-sum-exp consumed by vggt_attention_bwd.
-// Diagnostic: the default forward (variant 33, 32x32x16 form, the same 8- / 4-wave
-// choice as vggt_attention_fwd) with s_memtime segment stamps (VAR bit 1024).
+// Diagnostic: the default forward (variant 33 -- 2081 in the 8-wave form unless
+// VGGT_ATTN_DMA_HALF=0 --, 32x32x16 form, the same 8- / 4-wave choice as
+// vggt_attention_fwd) with s_memtime segment stamps (VAR bit 1024).
 extern "C" int vggt_attention_stamps(const void* q, int64_t ldq, int64_t q_bstride, const void* k, int64_t ldk,
                                      int64_t k_bstride, const void* v, int64_t ldv, int64_t v_bstride, void* o,
                                      int64_t ldo, int64_t o_bstride, unsigned long long* stamps, int batch, int heads,
@@ -1109,7 +1219,11 @@ extern "C" int vggt_attention_stamps(const void* q, int64_t ldq, int64_t q_bstri
   const int nw = (g_vggt_attn_waves == 8 && nq >= 4096) ? 8 : 4;
   const int nwg = ((nq + nw * 32 - 1) / (nw * 32)) * heads * batch;
   hipStream_t s = (hipStream_t)stream;
-  if (nw == 8) attn_fwd_kernel<64, 8, 33 | 1024><<<nwg, 512, 0, s>>>(a);
+  static const bool dma_half = getenv("VGGT_ATTN_DMA_HALF") ? atoi(getenv("VGGT_ATTN_DMA_HALF")) != 0 : true;
+  if (nw == 8 && (g_vggt_attn_variant == 2081 || (g_vggt_attn_variant == 33 && dma_half)))
+    attn_fwd_kernel<64, 8, 2081 | 1024><<<nwg, 512, 0, s>>>(a);
+  else if (nw == 8 && g_vggt_attn_variant == 4129) attn_fwd_kernel<64, 8, 4129 | 1024><<<nwg, 512, 0, s>>>(a);
+  else if (nw == 8) attn_fwd_kernel<64, 8, 33 | 1024><<<nwg, 512, 0, s>>>(a);
   else attn_fwd_kernel<64, 4, 33 | 1024><<<nwg, 256, 0, s>>>(a);
   HIP_LAUNCH_CHECK();
   return VGGT_OK;

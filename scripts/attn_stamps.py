@@ -32,8 +32,10 @@ def main():
     ap.add_argument("--heads", type=int, default=16)
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--warm-s", type=float, default=3.0)
+    ap.add_argument("--variant", type=int, default=33, help="VGGT_TUNE_ATTN_VARIANT: 33 (default), 2081, 4129")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
+    N.tune(N.TUNE_ATTN_VARIANT, a.variant)
     dev = torch.device("cuda:0")
     n, H, B, D = a.tokens, a.heads, a.batch, 64
     C = H * D
@@ -71,7 +73,7 @@ def main():
     tot = work + vm + bar
     nw = 8 if n >= 4096 else 4
     flops = 4.0 * B * H * n * n * D
-    res = {"shape": {"batch": B, "heads": H, "tokens": n, "D": D, "waves_per_workgroup": nw, "tiles_per_wave": nt},
+    res = {"variant": a.variant, "shape": {"batch": B, "heads": H, "tokens": n, "D": D, "waves_per_workgroup": nw, "tiles_per_wave": nt},
            "us_plain": round(us_plain, 1), "us_stamped": round(us_stamp, 1),
            "tflops_plain": round(flops / us_plain / 1e6, 1), "outputs_bitwise_equal": same,
            "cycles_per_tile": {"work": round(work.mean().item() / nt, 1), "vmcnt_wait": round(vm.mean().item() / nt, 1),
