@@ -645,57 +645,63 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
     if (t1 < nt) run(std::false_type{}, t1);
   } else if constexpr (VAR & 8192) {
     // Asynchronous ring (8-wave form with the DMA on the priority half, VAR & 2048):
-    // no per-tile barrier.  Three K|V slots; two LDS counters replace it:
-    //   landed: each issuing wave (4-7) adds 1 once its pieces of tile j >= 2 are in
-    //           LDS (counted vmcnt, tile j+1's pieces may stay in flight), so tile j
-    //           is readable once landed >= 4 (j - 1) (tiles 0 / 1: the prologue barrier);
-    //   done:   every wave adds 1 after its last LDS read of tile j, so the slot of
-    //           tile t-1 may take tile t+2's DMA once done >= 8 t.
-    // A wave may thus run up to one tile ahead of the slowest wave of its workgroup
+    // no per-tile barrier.  Three K|V slots; per-wave progress words in LDS replace it
+    // (one word per writer, so "every wave got here" is a min over the words -- a
+    // shared counter would let a wave that ran ahead stand in for one left behind):
+    //   full[w] (issuing waves 4-7): tiles j >= 2 whose pieces of w are in LDS (a
+    //           counted vmcnt: tile j+1's pieces may stay in flight); tile t is
+    //           readable once every full[w] >= t - 1 (tiles 0 / 1: the prologue barrier);
+    //   free[w] (all 8 waves): tiles whose LDS reads w has retired (lgkmcnt(0)); the
+    //           slot of tile t-1 may take tile t+2's DMA once every free[w] >= t.
+    // A wave may thus run ahead of the slowest one of its workgroup by up to a tile
     // (the segment stamps: the priority waves finished each tile ~870 cycles early
-    // and waited at the barrier).  Every wait depends only on strictly earlier
-    // tiles' signals, and is bounded: a lost signal ends in wrong output (the tests
-    // compare against fp32 torch), not in a hung wave.
+    // and waited at the barrier).  Every wait depends only on earlier tiles' words
+    // and is bounded: a lost word ends in wrong output (the tests compare against
+    // torch / an fp64 reference), not in a hung wave.
     static_assert(!(VAR & 8192) || DMAH, "the asynchronous ring needs the DMA on the priority half");
-    __shared__ uint32_t ctr[2];
+    __shared__ uint32_t full[4], freew[8];
     constexpr int P = 2 * IPWX;  // pieces per tile per issuing wave (K and V)
     const bool issuer = wave >= 4;
-    if (threadIdx.x == 0) {
-      ctr[0] = 0;
-      ctr[1] = 0;
-    }
+    if (threadIdx.x < 12) (threadIdx.x < 4 ? full[threadIdx.x] : freew[threadIdx.x - 4]) = 0;
     if (issuer) {
       stage(0, 0);
       if (nt > 1) stage(1, 1);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    auto wait_ge = [&](int idx, uint32_t target) {
+    auto min_of = [&](uint32_t* w, auto nc) -> uint32_t {
+      uint32_t m = __hip_atomic_load(&w[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+      for (int i = 1; i < decltype(nc)::value; ++i)
+        m = min(m, __hip_atomic_load(&w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+      return __builtin_amdgcn_readfirstlane(m);
+    };
+    auto wait_min = [&](uint32_t* w, auto nc, uint32_t target) {
       for (uint32_t spins = 0; spins < (1u << 22); ++spins) {
-        const uint32_t v = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(&ctr[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (v >= target) break;
+        if (min_of(w, nc) >= target) break;
         __builtin_amdgcn_s_sleep(1);
       }
-      asm volatile("" ::: "memory");  // the tile's LDS reads stay after the poll
+      asm volatile("" ::: "memory");  // the tile's LDS reads / DMA stay after the poll
     };
-    auto signal = [&](int idx) {
-      if (lane == 0) __hip_atomic_fetch_add(&ctr[idx], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    auto publish = [&](uint32_t* word, uint32_t v) {
+      if (lane == 0) __hip_atomic_store(word, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
+    using C4 = std::integral_constant<int, 4>;
+    using C8 = std::integral_constant<int, 8>;
     auto step = [&](auto sc, auto sf, auto zc, int t) {
-      if (t >= 2) wait_ge(0, 4u * (uint32_t)(t - 1));  // tile t landed
+      if (t >= 2) wait_min(full, C4{}, (uint32_t)(t - 1));  // tile t landed (every issuer's pieces)
       if (issuer && t + 2 < nt) {
-        wait_ge(1, 8u * (uint32_t)t);  // every wave is done with tile t-1's slot
+        wait_min(freew, C8{}, (uint32_t)t);  // every wave is done with tile t-1's slot
         stage(decltype(sf)::value, t + 2);
       }
       soft_pv(sc, t, qk(sc), zc);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot t done
-      signal(1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot t retired
+      publish(&freew[wave], (uint32_t)(t + 1));
       if (issuer && t + 1 >= 2 && t + 1 < nt) {
         // tile t+1's pieces (issued at the start of tile t-1) landed; t+2's may fly on
         if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        signal(0);
+        publish(&full[wave - 4], (uint32_t)t);
       }
     };
     auto run = [&](auto zc, int t0) -> int {
