@@ -444,6 +444,13 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
     if constexpr (!(VAR & 8)) l_run += (rs[0] + rs[1]) + (rs[2] + rs[3]);
     }
     // ---- O^T += V^T . P^T
+    // VAR & (16384 | 32768) (8-wave form): the priority-0 half (waves 0-3) raises its
+    // priority to 1 (16384) or 2 (32768) for the rest of the tile -- its P.V and the
+    // tile end -- and drops it back at the next tile's start (the stamps: it is the
+    // tile's critical path, ~870 cycles behind its priority-1 partner)
+    if constexpr (NW == 8 && (VAR & (16384 | 32768))) {
+      if (wave < 4) __builtin_amdgcn_s_setprio((VAR & 32768) ? 2 : 1);
+    }
 #pragma unroll
     for (int db = 0; db < NDB; ++db)
 #pragma unroll
@@ -735,6 +742,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
     auto run = [&](auto zc, int t0) -> int {
       for (int t = t0; t < nt; t += 2) {
         VGGT_SEG(-1);
+        if constexpr (NW == 8 && (VAR & (16384 | 32768))) {
+          if (wave < 4) __builtin_amdgcn_s_setprio(0);
+        }
         if (t + 1 < nt) stage(1, t + 1);
         if ((VAR & 256) && (t + 1) * BKV <= a.nk) tile_split(I0{}, zc);
         else soft_pv(I0{}, t, qk(I0{}), zc);
@@ -744,6 +754,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
         __syncthreads();
         VGGT_SEG(4);
         if (t + 1 >= nt) break;
+        if constexpr (NW == 8 && (VAR & (16384 | 32768))) {
+          if (wave < 4) __builtin_amdgcn_s_setprio(0);
+        }
         if (t + 2 < nt) stage(0, t + 2);
         if ((VAR & 256) && (t + 2) * BKV <= a.nk) tile_split(I1{}, zc);
         else soft_pv(I1{}, t + 1, qk(I1{}), zc);
@@ -1133,6 +1146,14 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
   static const bool dma_half = getenv("VGGT_ATTN_DMA_HALF") ? atoi(getenv("VGGT_ATTN_DMA_HALF")) != 0 : true;
   if (dma_half && g_vggt_attn_variant == 33 && D == 64 && nw == 8 && !a.lse) {
     attn_fwd_kernel<64, 8, 2081><<<nwg, 512, 0, s>>>(a);
+    HIP_LAUNCH_CHECK();
+    return VGGT_OK;
+  }
+  if ((g_vggt_attn_variant == 18465 || g_vggt_attn_variant == 34849) && D == 64 && nw != 2 && !a.lse) {
+    // 2081 with the priority-0 half raised for the second part of each tile (8-wave form)
+    if (nw == 8 && g_vggt_attn_variant == 18465) attn_fwd_kernel<64, 8, 18465><<<nwg, 512, 0, s>>>(a);
+    else if (nw == 8) attn_fwd_kernel<64, 8, 34849><<<nwg, 512, 0, s>>>(a);
+    else attn_fwd_kernel<64, 4, 33><<<nwg, 256, 0, s>>>(a);
     HIP_LAUNCH_CHECK();
     return VGGT_OK;
   }
