@@ -3,5 +3,5 @@
 set -u
 O=gpurun_out/r11g; mkdir -p $O
 timeout -k 10 600 python -u scripts/gemmbench.py --tokens 6608 --shapes qkv,proj,fc1,fc2 --epis torch,plain,gelu,resid \
-  --modes -1,0,1,2,3,4,5,6,7,8,9 --reps 50 > $O/gemm6608_modes.txt 2>&1 || { tail -20 $O/gemm6608_modes.txt; exit 1; }
+  --modes=-1,0,1,2,3,4,5,6,7,8,9 --reps 50 > $O/gemm6608_modes.txt 2>&1 || { tail -20 $O/gemm6608_modes.txt; exit 1; }
 grep -v '^{' $O/gemm6608_modes.txt | grep -v amdgpu.ids

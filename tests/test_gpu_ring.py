@@ -1,9 +1,10 @@
 """The multi-GPU chunk pipeline's W > 1 ring (dist/pipeline.py ``_run_ring``)
-carrying the real HIP model: two ranks on the one GPU of the test box (gloo
+carrying the real HIP model: two (or four) ranks on the one GPU of the test box (gloo
 process group; each baton and the end-of-sequence all-gather are staged
 through host memory, the rest -- encodes on the compute stream, alignment on
 the high-priority side stream, graphs, per-stream workspaces -- is the RCCL
-path's).  Both ranks must return the single-process chunk loop's results
+path's); also four ranks with the planner's offload placement.  Every rank
+must return the single-process chunk loop's results
 (training_metrics.py:616-659)."""
 import os
 import socket
@@ -36,7 +37,7 @@ def _model():
     return m.cuda().eval()
 
 
-def _worker(rank, world, port, q, shift=None):
+def _worker(rank, world, port, q, shift=None, offload=False):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "large-scale-vit-slam_amd")]
@@ -49,6 +50,7 @@ def _worker(rank, world, port, q, shift=None):
         m = _model()
         imgs = synthetic_images(1, N_FRAMES, H, W, seed=4).cuda()
         pipe = ChunkPipeline(m, device=torch.device("cuda"), gather_dense=True, time_align=True)
+        pipe.plan_offload = offload  # the planner's own placement of moved alignments (VGGT_RING_OFFLOAD=1)
         if shift is not None:  # every alignment away from its owner: the shipped prefix rows path
             from aligned_vggt.utils.data import generate_chunks
             n = len(generate_chunks(N_FRAMES, "chunk_overlap", W_CHUNK, OV))
@@ -56,16 +58,20 @@ def _worker(rank, world, port, q, shift=None):
         P1 = 6 + (H // 14) * (W // 14)
         out = pipe.run(imgs, W_CHUNK, OV, token_dims=(P1, 1024), memory_shape=(1, 8, 512))
         torch.cuda.synchronize()
-        q.put((rank, {k: v.cpu().numpy().copy() for k, v in out.items()}, pipe.align_ms()))
+        ar = tuple(pipe._last_plans[0].align_rank) if pipe.__dict__.get("_last_plans") else ()
+        q.put((rank, {k: v.cpu().numpy().copy() for k, v in out.items()}, pipe.align_ms(), ar))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("shift", [None, 1])
-def test_ring_two_ranks_real_model_matches_loop(shift):
+@pytest.mark.parametrize("world,shift,offload", [(2, None, False), (2, 1, False), (4, None, True)])
+def test_ring_two_ranks_real_model_matches_loop(world, shift, offload):
     """shift 1: every chunk's alignment runs on the other rank (its encode's
     alignment-head prefix rows and camera pose encoding shipped there, the
-    depth maps scaled by the owner after the gather)."""
+    depth maps scaled by the owner after the gather).  world 4 + offload
+    (ADVICE r5): four ranks with the planner's OWN placement of moved
+    alignments (7 chunks: 5 alignments move), so ships and batons between
+    the same rank pairs interleave as they would on a node."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     import torch.multiprocessing as mp
@@ -80,14 +86,21 @@ def test_ring_two_ranks_real_model_matches_loop(shift):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, shift)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, shift, offload)) for r in range(world)]
     for p in procs:
         p.start()
-    got = [q.get(timeout=240) for _ in range(2)]
+    got = [q.get(timeout=240) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, out, ms in got:
+    ars = {ar for _, _, _, ar in got}
+    assert len(ars) == 1, ars  # every rank planned the same placement
+    ar = ars.pop()
+    if offload:
+        moved = [i for i, a in enumerate(ar) if a != i % world]
+        print("alignments moved off their owner:", moved, "placement", ar)
+        assert moved, ar
+    for rank, out, ms, _ in got:
         print(f"rank {rank}: align ms per own chunk {[round(x, 2) for x in ms]}")
         for k, b in ref.items():
             a = torch.from_numpy(out[k])
