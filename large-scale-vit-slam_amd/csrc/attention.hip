@@ -108,7 +108,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
   constexpr int RPI = 1024 / ROWB;       // rows per 1-KiB DMA instruction
   constexpr int CPR = ROWB / 16;         // 16-B chunks per row
   constexpr int IPW = TILEB / 1024 / NW;  // DMA instructions per wave per operand
-  constexpr int NSLOT = (VAR & (16 | 512 | 8192)) ? 3 : 2;  // K|V tile slots (3: pipelined QK^T / DMA two ahead / async ring)
+  constexpr int NSLOT = (VAR & (16 | 512)) ? 3 : 2;  // K|V tile slots (3: pipelined QK^T / DMA two ahead)
   __shared__ __attribute__((aligned(16))) char smem[NSLOT * 2 * TILEB];
 
   const int lane = threadIdx.x & 63;
@@ -444,13 +444,6 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
     if constexpr (!(VAR & 8)) l_run += (rs[0] + rs[1]) + (rs[2] + rs[3]);
     }
     // ---- O^T += V^T . P^T
-    // VAR & (16384 | 32768) (8-wave form): the priority-0 half (waves 0-3) raises its
-    // priority to 1 (16384) or 2 (32768) for the rest of the tile -- its P.V and the
-    // tile end -- and drops it back at the next tile's start (the stamps: it is the
-    // tile's critical path, ~870 cycles behind its priority-1 partner)
-    if constexpr (NW == 8 && (VAR & (16384 | 32768))) {
-      if (wave < 4) __builtin_amdgcn_s_setprio((VAR & 32768) ? 2 : 1);
-    }
 #pragma unroll
     for (int db = 0; db < NDB; ++db)
 #pragma unroll
@@ -650,82 +643,6 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
     };
     const int t1 = run(std::true_type{}, 0);
     if (t1 < nt) run(std::false_type{}, t1);
-  } else if constexpr (VAR & 8192) {
-    // Asynchronous ring (8-wave form with the DMA on the priority half, VAR & 2048):
-    // no per-tile barrier.  Three K|V slots; per-wave progress words in LDS replace it
-    // (one word per writer, so "every wave got here" is a min over the words -- a
-    // shared counter would let a wave that ran ahead stand in for one left behind):
-    //   full[w] (issuing waves 4-7): tiles j >= 2 whose pieces of w are in LDS (a
-    //           counted vmcnt: tile j+1's pieces may stay in flight); tile t is
-    //           readable once every full[w] >= t - 1 (tiles 0 / 1: the prologue barrier);
-    //   free[w] (all 8 waves): tiles whose LDS reads w has retired (lgkmcnt(0)); the
-    //           slot of tile t-1 may take tile t+2's DMA once every free[w] >= t.
-    // A wave may thus run ahead of the slowest one of its workgroup by up to a tile
-    // (the segment stamps: the priority waves finished each tile ~870 cycles early
-    // and waited at the barrier).  Every wait depends only on earlier tiles' words
-    // and is bounded: a lost word ends in wrong output (the tests compare against
-    // torch / an fp64 reference), not in a hung wave.
-    static_assert(!(VAR & 8192) || DMAH, "the asynchronous ring needs the DMA on the priority half");
-    __shared__ uint32_t full[4], freew[8];
-    constexpr int P = 2 * IPWX;  // pieces per tile per issuing wave (K and V)
-    const bool issuer = wave >= 4;
-    if (threadIdx.x < 12) (threadIdx.x < 4 ? full[threadIdx.x] : freew[threadIdx.x - 4]) = 0;
-    if (issuer) {
-      stage(0, 0);
-      if (nt > 1) stage(1, 1);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    auto min_of = [&](uint32_t* w, auto nc) -> uint32_t {
-      uint32_t m = __hip_atomic_load(&w[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-      for (int i = 1; i < decltype(nc)::value; ++i)
-        m = min(m, __hip_atomic_load(&w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-      return __builtin_amdgcn_readfirstlane(m);
-    };
-    auto wait_min = [&](uint32_t* w, auto nc, uint32_t target) {
-      for (uint32_t spins = 0; spins < (1u << 22); ++spins) {
-        if (min_of(w, nc) >= target) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-      asm volatile("" ::: "memory");  // the tile's LDS reads / DMA stay after the poll
-    };
-    auto publish = [&](uint32_t* word, uint32_t v) {
-      if (lane == 0) __hip_atomic_store(word, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    using C4 = std::integral_constant<int, 4>;
-    using C8 = std::integral_constant<int, 8>;
-    auto step = [&](auto sc, auto sf, auto zc, int t) {
-      if (t >= 2) wait_min(full, C4{}, (uint32_t)(t - 1));  // tile t landed (every issuer's pieces)
-      if (issuer && t + 2 < nt) {
-        wait_min(freew, C8{}, (uint32_t)t);  // every wave is done with tile t-1's slot
-        stage(decltype(sf)::value, t + 2);
-      }
-      soft_pv(sc, t, qk(sc), zc);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot t retired
-      publish(&freew[wave], (uint32_t)(t + 1));
-      if (issuer && t + 1 >= 2 && t + 1 < nt) {
-        // tile t+1's pieces (issued at the start of tile t-1) landed; t+2's may fly on
-        if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        publish(&full[wave - 4], (uint32_t)t);
-      }
-    };
-    auto run = [&](auto zc, int t0) -> int {
-      for (int t = t0; t < nt; t += 3) {
-        step(I0{}, I2{}, zc, t);
-        if (t + 1 >= nt) break;
-        step(I1{}, I0{}, zc, t + 1);
-        if (t + 2 >= nt) break;
-        step(I2{}, I1{}, zc, t + 2);
-        if constexpr (decltype(zc)::value) {
-          if (!zero_off) return t + 3;
-        }
-      }
-      return nt;
-    };
-    const int t1 = run(std::true_type{}, 0);
-    if (t1 < nt) run(std::false_type{}, t1);
   } else {
     stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -742,9 +659,6 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
     auto run = [&](auto zc, int t0) -> int {
       for (int t = t0; t < nt; t += 2) {
         VGGT_SEG(-1);
-        if constexpr (NW == 8 && (VAR & (16384 | 32768))) {
-          if (wave < 4) __builtin_amdgcn_s_setprio(0);
-        }
         if (t + 1 < nt) stage(1, t + 1);
         if ((VAR & 256) && (t + 1) * BKV <= a.nk) tile_split(I0{}, zc);
         else soft_pv(I0{}, t, qk(I0{}), zc);
@@ -754,9 +668,6 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(AttnArgs a) {
         __syncthreads();
         VGGT_SEG(4);
         if (t + 1 >= nt) break;
-        if constexpr (NW == 8 && (VAR & (16384 | 32768))) {
-          if (wave < 4) __builtin_amdgcn_s_setprio(0);
-        }
         if (t + 2 < nt) stage(0, t + 2);
         if ((VAR & 256) && (t + 2) * BKV <= a.nk) tile_split(I1{}, zc);
         else soft_pv(I1{}, t + 1, qk(I1{}), zc);
@@ -1146,20 +1057,6 @@ extern "C" int vggt_attention_fwd(const void* q, int64_t ldq, int64_t q_bstride,
   static const bool dma_half = getenv("VGGT_ATTN_DMA_HALF") ? atoi(getenv("VGGT_ATTN_DMA_HALF")) != 0 : true;
   if (dma_half && g_vggt_attn_variant == 33 && D == 64 && nw == 8 && !a.lse) {
     attn_fwd_kernel<64, 8, 2081><<<nwg, 512, 0, s>>>(a);
-    HIP_LAUNCH_CHECK();
-    return VGGT_OK;
-  }
-  if ((g_vggt_attn_variant == 18465 || g_vggt_attn_variant == 34849) && D == 64 && nw != 2 && !a.lse) {
-    // 2081 with the priority-0 half raised for the second part of each tile (8-wave form)
-    if (nw == 8 && g_vggt_attn_variant == 18465) attn_fwd_kernel<64, 8, 18465><<<nwg, 512, 0, s>>>(a);
-    else if (nw == 8) attn_fwd_kernel<64, 8, 34849><<<nwg, 512, 0, s>>>(a);
-    else attn_fwd_kernel<64, 4, 33><<<nwg, 256, 0, s>>>(a);
-    HIP_LAUNCH_CHECK();
-    return VGGT_OK;
-  }
-  if (g_vggt_attn_variant == 10273 && D == 64 && nw != 2 && !a.lse) {  // 2081 on the asynchronous ring (8-wave form)
-    if (nw == 8) attn_fwd_kernel<64, 8, 10273><<<nwg, 512, 0, s>>>(a);
-    else attn_fwd_kernel<64, 4, 33><<<nwg, 256, 0, s>>>(a);
     HIP_LAUNCH_CHECK();
     return VGGT_OK;
   }

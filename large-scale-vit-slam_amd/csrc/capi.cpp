@@ -50,12 +50,10 @@ extern "C" int vggt_tune(int knob, int value) {
       // 0-15: bit combinations of the max-tracking kernel; 19/23: pipelined QK^T;
       // 32/33 (+64 exact scores): offset-free softmax; 161 = 33 on the 16x16x32 MFMA shape (D = 64)
       // 289 = 33 with the split-tile in-wave pipeline (D = 64); 545 = 33 with 3 K|V slots, DMA two tiles ahead;
-      // 2081 = 33 with the LDS-DMA issued by the priority half of the 8-wave form; 4129 = 33 without the priority raise;
-      // 10273 = 2081 on an asynchronous 3-slot ring (LDS counters instead of the per-tile barrier);
-      // 18465 / 34849 = 2081 with waves 0-3 at priority 1 / 2 from each tile's P.V to its end
+      // 2081 = 33 with the LDS-DMA issued by the priority half of the 8-wave form; 4129 = 33 without the priority raise
+      // (an asynchronous ring and dynamic priorities were measured and removed: profiles/r11/ab_attn_dma_half.md)
       if (value < 0 || (value > 15 && value != 19 && value != 23 && value != 32 && value != 33 && value != 96 &&
-                        value != 97 && value != 161 && value != 289 && value != 545 && value != 2081 && value != 4129 &&
-                        value != 10273 && value != 18465 && value != 34849))
+                        value != 97 && value != 161 && value != 289 && value != 545 && value != 2081 && value != 4129))
         return VGGT_ERR_UNSUPPORTED;
       prev = g_vggt_attn_variant;
       g_vggt_attn_variant = value;

@@ -262,7 +262,7 @@ def _ref_attn(q, k, v, scale):
     return torch.softmax(s, -1) @ v.float()
 
 
-@pytest.mark.parametrize("variant", [3, 11, 15, 19, 23, 32, 97, 161, 289, 545, 2081, 4129, 10273, 18465, 34849])
+@pytest.mark.parametrize("variant", [3, 11, 15, 19, 23, 32, 97, 161, 289, 545, 2081, 4129])
 @pytest.mark.parametrize("D,H,batch,n", [(64, 16, 3, 21), (64, 16, 2, 1374), (128, 8, 2, 1375), (64, 2, 1, 4100),
                                          (128, 2, 1, 64), (64, 1, 1, 1)])
 def test_attention_vs_torch(N, D, H, batch, n, variant):
@@ -376,7 +376,7 @@ def test_attention_online_softmax_rescale(N, variant):
         N.tune(N.TUNE_ATTN_VARIANT, prev)
 
 
-@pytest.mark.parametrize("variant", [32, 33, 96, 97, 161, 289, 545, 2081, 4129, 10273, 18465, 34849])
+@pytest.mark.parametrize("variant", [32, 33, 96, 97, 161, 289, 545, 2081, 4129])
 @pytest.mark.parametrize("case", ["overflow_late", "all_negative", "huge_first_tile", "mixed_rows"])
 @pytest.mark.parametrize("waves,n", [(4, 700), (8, 4200)])
 def test_attention_offset_free_extremes(N, variant, case, waves, n):
