@@ -213,3 +213,41 @@ def test_collective_gather_over_rccl_world1(cuda, monkeypatch):
             assert torch.equal(got[k].cpu(), ref[k].cpu()), k
     finally:
         dist.destroy_process_group()
+
+
+def test_baton_p2p_batch_over_rccl_self():
+    """VERDICT r5 missing #3: the baton's ``batch_isend_irecv`` of P2POps on an
+    ``nccl`` (RCCL) group with DEVICE buffers, world size 1 -- the rank sends
+    the baton's tensors to itself, sends and receives in ONE batch (RCCL pairs
+    them in one group call), on the default group and on a second group made
+    like the pipeline's ship group (``use_local_synchronization=True``).  The
+    ring's two-device case stays for the driver's 8-GPU run."""
+    import socket
+
+    import torch.distributed as dist
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    assert not dist.is_initialized()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    try:
+        ship = dist.new_group(ranks=[0], backend="nccl", use_local_synchronization=True)
+        g = torch.Generator(device="cuda").manual_seed(0)
+        P1 = 6 + 11 * 37
+        baton = {"overlap_tokens": torch.randn(1, 5, P1, 1024, device=dev, generator=g),
+                 "pose_enc": torch.randn(1, 16, 9, device=dev, generator=g),
+                 "memory_tokens": torch.randn(1, 8, 512, device=dev, generator=g)}
+        for grp in (None, ship):
+            out = {k: torch.empty_like(v) for k, v in baton.items()}
+            ops = [dist.P2POp(dist.isend, t, 0, group=grp) for t in baton.values()]
+            ops += [dist.P2POp(dist.irecv, t, 0, group=grp) for t in out.values()]
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+            torch.cuda.synchronize()
+            for k in baton:
+                assert torch.equal(out[k], baton[k]), k
+    finally:
+        dist.destroy_process_group()
